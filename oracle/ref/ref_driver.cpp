@@ -1,0 +1,305 @@
+// Deterministic driver around the UNMODIFIED reference BDPT integrator.
+//
+// TEST INFRASTRUCTURE ONLY. This file is compiled together with the reference's
+// own sources under /root/reference (see oracle/ref/Makefile); the resulting
+// binary oracle/_ref/ref_bdpt is used to (a) generate the golden fixtures under
+// tests/golden/ and (b) time the reference CPU path as bench.py's cpu_baseline.
+// It is never linked into, or called by, the product library.
+//
+// What it restates: the offline branch of Renderer::render
+// (reference src/core/renderer.cpp:130-214) with ONE change that the survey's
+// parity convention requires: instead of one Sampler shared
+// racily by all threads (renderer.cpp:155, :159), every (pixel p, sample k)
+// gets its own Sampler((int)(260450963u + p*spp + k)). BDPTIntegrator::render
+// (src/integrators/bdpt.h:219) and everything below it are the reference's code,
+// unchanged.
+//
+// Modes:
+//   ref_bdpt render <scene.toml> W H SPP [--rr D] [--threads T]
+//                   [--row-stride S --row-offset O] [--out fb.f32]
+//   ref_bdpt sample <scene.toml> W H SPP P K      (one sample: Li + splat list)
+//   ref_bdpt dump   <scene.toml> W H OUTDIR       (scene / BVH / camera dump)
+
+#define main tinyrender_reference_main
+#include "main.cpp"   // reference src/main.cpp: loadTOML, g_FrameBufferLocks, tinyobj/tinyexr impl
+#undef main
+
+#include <integrators/bdpt.h>
+#include <bsdfs/mixture.h>
+#include <bsdfs/glass.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+using namespace TinyRender;
+
+namespace {
+
+struct Cam {
+    glm::mat4 worldToCamera, cameraToWorld, cameraToClip, NDCToScreen;
+    float invWidth, invHeight, angle, aspectRatio;
+};
+
+// renderer.cpp:140-153, verbatim semantics.
+Cam makeCam(const Config& cfg, int W, int H) {
+    Cam c;
+    const float near = 1.f, far = 1000.f;
+    c.worldToCamera = glm::lookAt(cfg.camera.o, cfg.camera.at, cfg.camera.up);
+    c.cameraToWorld = glm::inverse(c.worldToCamera);
+    c.invWidth = 1.f / W;
+    c.invHeight = 1.f / H;
+    c.angle = std::tanf(deg2rad * cfg.camera.fov * 0.5f);
+    c.aspectRatio = (float)W / H;
+    c.cameraToClip = glm::perspective(deg2rad * cfg.camera.fov, c.aspectRatio, near, far);
+    c.NDCToScreen = glm::scale(glm::mat4(1.f), v3f(W, H, 1.0f)) * glm::scale(glm::mat4(1.f), v3f(0.5f, -0.5f, 1.f)) *
+                    glm::translate(glm::mat4(1.f), v3f(1.f, -1.f, 0.f));
+    return c;
+}
+
+// One camera sample exactly as renderer.cpp:165-195 builds it.
+Ray cameraRay(const Config& cfg, const Cam& c, int W, int spp, int pixel, Sampler& sampler) {
+    const float near = 1.f, far = 1000.f;
+    int j = pixel % W;
+    int i = pixel / W;
+    float y = (1.f - ((float)i + 0.5f) * c.invHeight) * 2.f - 1.f;
+    float x = (((float)j + 0.5f) * c.invWidth) * 2.f - 1.f;
+    v4f imagePlanePoint;
+    if (spp == 1) {
+        imagePlanePoint = v4f(x * c.angle * c.aspectRatio, y * c.angle, -near, 0);
+    } else {
+        p2f randomSample = sampler.next2D();
+        randomSample -= 0.5f;
+        randomSample.x = randomSample.x * c.invWidth;
+        randomSample.y = randomSample.y * c.invHeight;
+        imagePlanePoint = v4f((x + randomSample.x) * c.angle * c.aspectRatio, (y + randomSample.y) * c.angle, -near, 0);
+    }
+    v3f rayDir = c.cameraToWorld * imagePlanePoint;
+    rayDir = glm::normalize(rayDir);
+    return Ray(cfg.camera.o, rayDir, near, far);
+}
+
+inline int seedFor(int pixel, int spp, int k) {
+    return (int)(260450963u + (unsigned)pixel * (unsigned)spp + (unsigned)k);
+}
+
+struct Setup {
+    Config cfg;
+    std::unique_ptr<Scene> scene;
+    std::unique_ptr<BDPTIntegrator> integ;
+};
+
+void setup(Setup& s, const std::string& toml, int W, int H, int spp, int rr) {
+    loadTOML(s.cfg, toml);
+    s.cfg.width = W;
+    s.cfg.height = H;
+    s.cfg.spp = spp;
+    if (rr > 0) s.cfg.integratorSettings.pt.rrDepth = rr;
+    std::cout.setstate(std::ios::failbit);  // silence the reference's progress prints
+    s.scene.reset(new Scene(s.cfg));
+    if (!s.scene->load(false)) { std::cout.clear(); fprintf(stderr, "scene load failed\n"); exit(2); }
+    s.integ.reset(new BDPTIntegrator(*s.scene));
+    s.integ->init();
+    std::cout.clear();
+    g_FrameBufferLocks.reset(new std::mutex[(size_t)W * H]);
+}
+
+int cmdRender(int argc, char** argv) {
+    std::string toml = argv[2];
+    int W = atoi(argv[3]), H = atoi(argv[4]), spp = atoi(argv[5]);
+    int rr = 0, threads = 1, rowStride = 1, rowOffset = 0;
+    std::string out;
+    for (int a = 6; a < argc; a++) {
+        std::string k = argv[a];
+        if (k == "--rr") rr = atoi(argv[++a]);
+        else if (k == "--threads") threads = atoi(argv[++a]);
+        else if (k == "--row-stride") rowStride = atoi(argv[++a]);
+        else if (k == "--row-offset") rowOffset = atoi(argv[++a]);
+        else if (k == "--out") out = argv[++a];
+        else { fprintf(stderr, "unknown arg %s\n", k.c_str()); return 2; }
+    }
+    Setup s;
+    setup(s, toml, W, H, spp, rr);
+    Cam cam = makeCam(s.cfg, W, H);
+    std::vector<int> rows;
+    for (int r = rowOffset; r < H; r += rowStride) rows.push_back(r);
+    std::atomic<size_t> next(0);
+    auto worker = [&]() {
+        for (;;) {
+            size_t ri = next.fetch_add(1);
+            if (ri >= rows.size()) break;
+            int row = rows[ri];
+            for (int j = 0; j < W; j++) {
+                int pixel = row * W + j;
+                v3f averageRadiance(0.f);
+                for (int k = 0; k < spp; k++) {
+                    Sampler sampler(seedFor(pixel, spp, k));
+                    Ray ray = cameraRay(s.cfg, cam, W, spp, pixel, sampler);
+                    averageRadiance += s.integ->render(ray, sampler);
+                }
+                std::mutex& lock = g_FrameBufferLocks[pixel];
+                lock.lock();
+                s.integ->rgb->data[pixel] += averageRadiance * (1.f / spp);
+                lock.unlock();
+            }
+        }
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
+    double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    double samples = (double)rows.size() * W * spp;
+    if (!out.empty()) {
+        FILE* f = fopen(out.c_str(), "wb");
+        fwrite(&s.integ->rgb->data[0], sizeof(float), (size_t)W * H * 3, f);
+        fclose(f);
+    }
+    printf("{\"samples\": %.0f, \"seconds\": %.6f, \"msamples_per_s\": %.6f, \"threads\": %d, \"rr_depth\": %d}\n",
+           samples, sec, samples / sec * 1e-6, threads, s.integ->m_rrDepth);
+    return 0;
+}
+
+int cmdSample(int argc, char** argv) {
+    if (argc < 8) return 2;
+    std::string toml = argv[2];
+    int W = atoi(argv[3]), H = atoi(argv[4]), spp = atoi(argv[5]), P = atoi(argv[6]), K = atoi(argv[7]);
+    Setup s;
+    setup(s, toml, W, H, spp, argc > 8 ? atoi(argv[8]) : 0);
+    Cam cam = makeCam(s.cfg, W, H);
+    Sampler sampler(seedFor(P, spp, K));
+    Ray ray = cameraRay(s.cfg, cam, W, spp, P, sampler);
+    v3f Li = s.integ->render(ray, sampler);
+    printf("ray %a %a %a | %a %a %a\n", ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z);
+    printf("Li %a %a %a\n", Li.x, Li.y, Li.z);
+    for (int p = 0; p < W * H; p++) {
+        v3f v = s.integ->rgb->data[p];
+        if (v.x != 0.f || v.y != 0.f || v.z != 0.f) printf("splat %d %a %a %a\n", p, v.x, v.y, v.z);
+    }
+    return 0;
+}
+
+void writeBin(const std::string& path, const void* data, size_t bytes) {
+    FILE* f = fopen(path.c_str(), "wb");
+    fwrite(data, 1, bytes, f);
+    fclose(f);
+}
+
+int cmdDump(int argc, char** argv) {
+    std::string toml = argv[2];
+    int W = atoi(argv[3]), H = atoi(argv[4]);
+    std::string dir = argv[5];
+    Setup s;
+    setup(s, toml, W, H, 1, 0);
+    const Scene& sc = *s.scene;
+    const WorldData& wd = sc.worldData;
+
+    // Triangles in BVH leaf order (AcceleratorBVH::objects is reordered in place
+    // by BVH::build, so it IS the build_prims order the flat tree indexes).
+    std::vector<float> tf;
+    std::vector<int> ti;
+    for (Object* o : sc.bvh->objects) {
+        auto* n = (AcceleratorBVH::BVHNode*)o;
+        const tinyobj::mesh_t& m = wd.shapes[n->shapeID].mesh;
+        for (int c = 0; c < 3; c++) {
+            const tinyobj::index_t& ix = m.indices[n->faceID + c];
+            for (int d = 0; d < 3; d++) tf.push_back(wd.attrib.vertices[3 * ix.vertex_index + d]);
+        }
+        for (int c = 0; c < 3; c++) {
+            const tinyobj::index_t& ix = m.indices[n->faceID + c];
+            for (int d = 0; d < 3; d++) tf.push_back(wd.attrib.normals[3 * ix.normal_index + d]);
+        }
+        ti.push_back((int)n->shapeID);
+        ti.push_back((int)(n->faceID / 3));
+        ti.push_back(m.material_ids[n->faceID / 3]);
+    }
+    writeBin(dir + "/tri_f32.bin", tf.data(), tf.size() * 4);
+    writeBin(dir + "/tri_i32.bin", ti.data(), ti.size() * 4);
+
+    // Flat BVH nodes in preorder: count by walking from the root.
+    const BVHFlatNode* ft = sc.bvh->bvh->flatTree;
+    std::vector<uint32_t> stack{0};
+    uint32_t maxIdx = 0;
+    while (!stack.empty()) {
+        uint32_t ni = stack.back();
+        stack.pop_back();
+        if (ni > maxIdx) maxIdx = ni;
+        if (ft[ni].rightOffset != 0) {
+            stack.push_back(ni + 1);
+            stack.push_back(ni + ft[ni].rightOffset);
+        }
+    }
+    std::vector<float> nb;
+    std::vector<uint32_t> ni3;
+    for (uint32_t i = 0; i <= maxIdx; i++) {
+        const BBox& b = ft[i].bbox;
+        float v[6] = {b.min.x, b.min.y, b.min.z, b.max.x, b.max.y, b.max.z};
+        nb.insert(nb.end(), v, v + 6);
+        ni3.push_back(ft[i].start);
+        ni3.push_back(ft[i].nPrims);
+        ni3.push_back(ft[i].rightOffset);
+    }
+    writeBin(dir + "/node_f32.bin", nb.data(), nb.size() * 4);
+    writeBin(dir + "/node_u32.bin", ni3.data(), ni3.size() * 4);
+
+    // Camera constants (renderer.cpp:140-153; bdpt.h:49-54, :485-489).
+    Cam cam = makeCam(s.cfg, W, H);
+    std::vector<float> cf;
+    for (const glm::mat4* m : {&cam.worldToCamera, &cam.cameraToWorld, &cam.cameraToClip, &cam.NDCToScreen})
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 4; r++) cf.push_back((*m)[c][r]);
+    v3f fwd = glm::normalize(s.cfg.camera.at - s.cfg.camera.o);
+    float vnear = (1.f / std::tanf(deg2rad * s.cfg.camera.fov * 0.5f)) * H * 0.5f;
+    float extra[] = {cam.invWidth, cam.invHeight, cam.angle, cam.aspectRatio, fwd.x, fwd.y, fwd.z, vnear};
+    cf.insert(cf.end(), extra, extra + 8);
+    writeBin(dir + "/camera_f32.bin", cf.data(), cf.size() * 4);
+
+    // Materials: parsed MTL values plus the BSDF constructors' derived constants.
+    FILE* f = fopen((dir + "/materials.txt").c_str(), "w");
+    for (size_t i = 0; i < wd.materials.size(); i++) {
+        const tinyobj::material_t& m = wd.materials[i];
+        float scale = 1.f, specW = 0.f;
+        if (auto* mx = dynamic_cast<const MixtureBSDF*>(sc.bsdfs[i].get())) { scale = mx->scale; specW = mx->specularSamplingWeight; }
+        fprintf(f, "%zu %d %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %s\n", i, m.illum,
+                m.diffuse[0], m.diffuse[1], m.diffuse[2], m.specular[0], m.specular[1], m.specular[2],
+                m.emission[0], m.emission[1], m.emission[2], m.transmittance[0], m.transmittance[1], m.transmittance[2],
+                m.shininess, m.ior, scale, specW, 0.f, 0.f, 0.f, 0.f, m.name.c_str());
+    }
+    fclose(f);
+    f = fopen((dir + "/emitters.txt").c_str(), "w");
+    for (const Emitter& e : sc.emitters) {
+        fprintf(f, "%zu %a %a %a %a %zu", e.shapeID, e.area, e.radiance.x, e.radiance.y, e.radiance.z,
+                e.faceAreaDistribution.cdf.size());
+        for (float c : e.faceAreaDistribution.cdf) fprintf(f, " %a", c);
+        fprintf(f, "\n");
+    }
+    fclose(f);
+    f = fopen((dir + "/shapes.txt").c_str(), "w");
+    for (size_t i = 0; i < wd.shapes.size(); i++)
+        fprintf(f, "%zu %zu %s\n", i, wd.shapes[i].mesh.indices.size() / 3, wd.shapes[i].name.c_str());
+    fclose(f);
+    printf("{\"triangles\": %zu, \"nodes\": %u, \"shapes\": %zu, \"materials\": %zu, \"emitters\": %zu}\n",
+           sc.bvh->objects.size(), maxIdx + 1, wd.shapes.size(), wd.materials.size(), sc.emitters.size());
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        fprintf(stderr, "usage: ref_bdpt render|sample|dump <scene.toml> ...\n");
+        return 2;
+    }
+    std::string cmd = argv[1];
+    if (cmd == "render" && argc >= 6) return cmdRender(argc, argv);
+    if (cmd == "sample") return cmdSample(argc, argv);
+    if (cmd == "dump" && argc >= 6) return cmdDump(argc, argv);
+    fprintf(stderr, "bad command\n");
+    return 2;
+}
