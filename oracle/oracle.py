@@ -1,0 +1,163 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding for the C oracle (oracle/src).
+
+Used by tests/ (as the checker), __graft_entry__.smoke() and bench.py's
+cpu_baseline leg. Never imported by the product package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+REF_BIN = os.path.join(HERE, "_ref", "ref_bdpt")
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("eye", ctypes.c_float * 3),
+        ("at", ctypes.c_float * 3),
+        ("up", ctypes.c_float * 3),
+        ("fov", ctypes.c_float),
+        ("width", ctypes.c_int),
+        ("height", ctypes.c_int),
+        ("spp", ctypes.c_int),
+        ("rr_depth", ctypes.c_int),
+    ]
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.tro_scene_load.restype = ctypes.c_void_p
+        L.tro_scene_load.argtypes = [ctypes.c_char_p]
+        L.tro_scene_free.argtypes = [ctypes.c_void_p]
+        L.tro_last_error.restype = ctypes.c_char_p
+        L.tro_scene_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+        L.tro_scene_dump.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 4
+        L.tro_camera.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p]
+        L.tro_render.restype = ctypes.c_int64
+        L.tro_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_void_p,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.tro_sample.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_void_p, ctypes.c_void_p]
+        L.tro_counters.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+        L.tro_mt19937_nth.restype = ctypes.c_uint32
+        L.tro_mt19937_nth.argtypes = [ctypes.c_uint32, ctypes.c_int]
+        L.tro_sampler_nth.restype = ctypes.c_float
+        L.tro_sampler_nth.argtypes = [ctypes.c_uint32, ctypes.c_int]
+        for fn in ("tro_sinf", "tro_cosf"):
+            getattr(L, fn).restype = ctypes.c_float
+            getattr(L, fn).argtypes = [ctypes.c_float]
+        L.tro_powf.restype = ctypes.c_float
+        L.tro_powf.argtypes = [ctypes.c_float, ctypes.c_float]
+        _lib = L
+    return _lib
+
+
+def make_params(cam: dict, width: int, height: int, spp: int, rr_depth: int) -> Params:
+    p = Params()
+    p.eye[:] = [float(x) for x in cam["eye"]]
+    p.at[:] = [float(x) for x in cam["at"]]
+    p.up[:] = [float(x) for x in cam["up"]]
+    p.fov = float(cam["fov"])
+    p.width, p.height, p.spp, p.rr_depth = width, height, spp, rr_depth
+    return p
+
+
+class Scene:
+    def __init__(self, obj_path: str):
+        L = lib()
+        self._h = L.tro_scene_load(obj_path.encode())
+        if not self._h:
+            raise RuntimeError("oracle scene load failed: " + L.tro_last_error().decode())
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().tro_scene_free(self._h)
+            self._h = None
+
+    def stats(self) -> dict:
+        out = (ctypes.c_int64 * 6)()
+        lib().tro_scene_stats(self._h, out)
+        return dict(zip(["triangles", "nodes", "shapes", "materials", "emitters", "max_depth"], list(out)))
+
+    def dump(self):
+        st = self.stats()
+        nt, nn = st["triangles"], st["nodes"]
+        tf = np.zeros((nt, 18), np.float32)
+        ti = np.zeros((nt, 3), np.int32)
+        nf = np.zeros((nn, 6), np.float32)
+        nu = np.zeros((nn, 3), np.uint32)
+        lib().tro_scene_dump(self._h, tf.ctypes.data, ti.ctypes.data, nf.ctypes.data, nu.ctypes.data)
+        return tf, ti, nf, nu
+
+    def render(self, p: Params, threads: int = 1, rows: list[int] | None = None) -> tuple[np.ndarray, int]:
+        """Returns (framebuffer [H*W*3] float32, samples). threads > 1 splits
+        rows round-robin over threads with private framebuffers summed at the
+        end (same per-sample work; splat sums reassociate)."""
+        L = lib()
+        W, H = p.width, p.height
+        if rows is None:
+            rows = list(range(H))
+        if threads <= 1:
+            fb = np.zeros(W * H * 3, np.float32)
+            n = 0
+            # contiguous single-threaded pass in pixel order == reference order
+            if rows == list(range(H)):
+                n = L.tro_render(self._h, ctypes.byref(p), fb.ctypes.data, 0, H, 1)
+            else:
+                for r in rows:
+                    n += L.tro_render(self._h, ctypes.byref(p), fb.ctypes.data, r, r + 1, 1)
+            return fb, n
+        fbs = [np.zeros(W * H * 3, np.float32) for _ in range(threads)]
+        counts = [0] * threads
+
+        def work(t):
+            for r in rows[t::threads]:
+                counts[t] += L.tro_render(self._h, ctypes.byref(p), fbs[t].ctypes.data, r, r + 1, 1)
+
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        fb = fbs[0]
+        for f in fbs[1:]:
+            fb += f
+        return fb, sum(counts)
+
+    def sample(self, p: Params, pixel: int, k: int):
+        fb = np.zeros(p.width * p.height * 3, np.float32)
+        Li = np.zeros(3, np.float32)
+        lib().tro_sample(self._h, ctypes.byref(p), pixel, k, Li.ctypes.data, fb.ctypes.data)
+        return Li, fb
+
+
+def camera(p: Params) -> np.ndarray:
+    out = np.zeros(72, np.float32)
+    lib().tro_camera(ctypes.byref(p), out.ctypes.data)
+    return out
+
+
+def counters(reset: bool = True) -> dict:
+    out = (ctypes.c_int64 * 8)()
+    lib().tro_counters(out, 1 if reset else 0)
+    keys = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
+            "light_vert_reads", "splats", "rng_draws"]
+    return dict(zip(keys, list(out)))
