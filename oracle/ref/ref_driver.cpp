@@ -95,12 +95,12 @@ struct Setup {
 };
 
 void setup(Setup& s, const std::string& toml, int W, int H, int spp, int rr) {
+    std::cout.setstate(std::ios::failbit);  // silence the reference's progress prints
     loadTOML(s.cfg, toml);
     s.cfg.width = W;
     s.cfg.height = H;
     s.cfg.spp = spp;
     if (rr > 0) s.cfg.integratorSettings.pt.rrDepth = rr;
-    std::cout.setstate(std::ios::failbit);  // silence the reference's progress prints
     s.scene.reset(new Scene(s.cfg));
     if (!s.scene->load(false)) { std::cout.clear(); fprintf(stderr, "scene load failed\n"); exit(2); }
     s.integ.reset(new BDPTIntegrator(*s.scene));

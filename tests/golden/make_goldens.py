@@ -1,0 +1,105 @@
+"""Generates the golden fixtures in tests/golden/ from the UNMODIFIED reference.
+
+Run in the development container (needs /root/reference):
+    make -C oracle/ref            # builds oracle/_ref/ref_bdpt from the reference sources
+    python tests/golden/make_goldens.py
+
+Every framebuffer fixture is the output of oracle/_ref/ref_bdpt (reference
+BDPTIntegrator::render + the per-(pixel, sample)-seeded driver of
+oracle/ref/ref_driver.cpp), single-threaded so splats land in the reference's
+own order. Scene fixtures are sha256 digests of the reference's triangle list
+(BVH leaf order), flat BVH nodes and camera matrices (ref_bdpt dump).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import platform
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "scenes"))
+import variants  # noqa: E402
+
+REF = os.path.join(REPO, "oracle", "_ref", "ref_bdpt")
+
+# name: (scene, W, H, spp, rrDepth, row_stride)
+FRAMEBUFFERS = {
+    "G1_cbox_low_64x64_spp4": ("cbox_low", 64, 64, 4, 5, 1),
+    "G2_caustic_64x64_spp16": ("caustic", 64, 64, 16, 8, 1),
+    "G3_hardlight_64x64_spp16": ("hardlight", 64, 64, 16, 2, 1),
+    "G4_hardlight_mirror_64x64_spp16": ("hardlight_mirror", 64, 64, 16, 5, 1),
+    "G5_caustic_80x48_spp1": ("caustic", 80, 48, 1, 8, 1),
+    # bench resolution: every 16th row of 512x512 at 4 spp (splats land everywhere)
+    "G6_caustic_512x512_spp4_rows16": ("caustic", 512, 512, 4, 8, 16),
+    "G7_hardlight_512x512_spp4_rows32": ("hardlight", 512, 512, 4, 2, 32),
+}
+
+SCENE_DUMPS = {"cbox_low": (64, 64), "caustic": (512, 512), "hardlight": (512, 512), "hardlight_mirror": (512, 512)}
+
+
+def sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+def main() -> None:
+    if not os.path.exists(REF):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle", "ref")], check=True)
+    manifest = {
+        "generator": "oracle/_ref/ref_bdpt (reference sources @ /root/reference, oracle/ref/Makefile)",
+        "compiler": subprocess.run(["g++", "--version"], capture_output=True, text=True).stdout.splitlines()[0],
+        "glibc": platform.libc_ver()[1],
+        "seed_convention": "Sampler((int)(260450963u + pixel*spp + k)); jitter next2D first when spp > 1",
+        "framebuffers": {},
+        "scenes": {},
+    }
+    tmp = tempfile.mkdtemp()
+    for name, (scene, W, H, spp, rr, stride) in FRAMEBUFFERS.items():
+        toml = os.path.join(tmp, name + ".toml")
+        with open(toml, "w") as f:
+            f.write(variants.toml_text(scene, W, H, spp, rr))
+        out = os.path.join(tmp, name + ".f32")
+        cmd = [REF, "render", toml, str(W), str(H), str(spp), "--rr", str(rr), "--out", out]
+        if stride > 1:
+            cmd += ["--row-stride", str(stride)]
+        r = subprocess.run(cmd, capture_output=True, text=True, check=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        fb = np.fromfile(out, np.float32)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), fb=fb)
+        manifest["framebuffers"][name] = dict(scene=scene, width=W, height=H, spp=spp, rr_depth=rr, row_stride=stride,
+                                              samples=info["samples"], sha256=sha(fb.tobytes()),
+                                              mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
+                                              ref_seconds=info["seconds"])
+        print(name, manifest["framebuffers"][name]["sha256"][:16], info)
+    for scene, (W, H) in SCENE_DUMPS.items():
+        toml = os.path.join(tmp, scene + "_dump.toml")
+        with open(toml, "w") as f:
+            f.write(variants.toml_text(scene, W, H, 1))
+        d = os.path.join(tmp, scene + "_dump")
+        os.makedirs(d, exist_ok=True)
+        r = subprocess.run([REF, "dump", toml, str(W), str(H), d], capture_output=True, text=True, check=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        ent = dict(info)
+        ent["width"], ent["height"] = W, H
+        for fn in ("tri_f32", "tri_i32", "node_f32", "node_u32", "camera_f32"):
+            with open(os.path.join(d, fn + ".bin"), "rb") as f:
+                ent[fn + "_sha256"] = sha(f.read())
+        cam = np.fromfile(os.path.join(d, "camera_f32.bin"), np.float32)
+        ent["camera_f32"] = [float(x).hex() for x in cam]
+        for fn in ("materials", "emitters", "shapes"):
+            with open(os.path.join(d, fn + ".txt")) as f:
+                ent[fn + "_txt"] = f.read().splitlines()
+        manifest["scenes"][scene] = ent
+        print(scene, info)
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
