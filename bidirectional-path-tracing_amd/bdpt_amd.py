@@ -1,0 +1,260 @@
+"""Python host binding of the MI355X BDPT library (lib/libbdpt_amd.so).
+
+Mirrors the reference's plugin surface for the BDPT path
+(JackMinn/Bidirectional-Path-Tracing):
+
+  Scene(obj_path)                      Scene::load          src/core/renderer.cpp:235-315
+  BDPTIntegrator(scene, config)        BDPTIntegrator ctor  src/integrators/bdpt.h:38-43
+    .init()                            Integrator::init     src/core/integrator.cpp:16-20 (allocates rgb)
+    .render(ray, sampler) -> Li        Integrator::render   bdpt.h:219-241 (one camera sample)
+    .render_frame(...)                 Renderer::render offline loop renderer.cpp:130-214
+    .rgb                               Integrator::rgb      (W x H x 3 float32, accumulated)
+  Sampler(seed)                        Sampler              src/core/math.h:63-76 (seed + draw count)
+  Ray(o, d, min_t, max_t)              Ray                  src/core/core.h:117-122
+
+Everything renders on the GPU through the C-ABI of include/bdpt_amd.h; there
+is no CPU fallback (a missing library or device raises).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libbdpt_amd.so")
+
+STRATEGY_BDPT, STRATEGY_LIGHT_TRACING, STRATEGY_PATH_TRACING = 0, 1, 2
+FLAG_COUNT, FLAG_FULL_TRAVERSAL = 1, 2
+REFERENCE_SEED = 260450963  # renderer.cpp:155
+COUNTER_NAMES = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
+                 "light_vert_reads", "splats", "rng_draws"]
+
+
+class BdptError(RuntimeError):
+    pass
+
+
+class _Camera(ctypes.Structure):
+    _fields_ = [("eye", ctypes.c_float * 3), ("at", ctypes.c_float * 3), ("up", ctypes.c_float * 3),
+                ("fov", ctypes.c_float)]
+
+
+class _FrameParams(ctypes.Structure):
+    _fields_ = [("camera", _Camera), ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+                ("rr_depth", ctypes.c_int32), ("strategy", ctypes.c_int32), ("seed_base", ctypes.c_uint32),
+                ("row_offset", ctypes.c_int32), ("row_stride", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class _SceneInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in
+                ("triangles", "bvh_nodes", "shapes", "materials", "emitters", "bvh_max_depth", "device_bytes")]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
+                ("counters", ctypes.c_int64 * 8)]
+
+
+def build(force: bool = False) -> str:
+    """Compiles lib/libbdpt_amd.so in-tree with hipcc for gfx950."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", HERE, "-j4"], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise BdptError(f"{LIB_PATH} is missing: run build() (hipcc --offload-arch=gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, f32p = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_float)
+        L.bdpt_last_error.restype = ctypes.c_char_p
+        L.bdpt_version.restype = ctypes.c_char_p
+        L.bdpt_scene_load_obj.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
+        L.bdpt_scene_free.argtypes = [vp]
+        L.bdpt_scene_get_info.argtypes = [vp, ctypes.POINTER(_SceneInfo)]
+        L.bdpt_scene_export.argtypes = [vp, vp, vp, vp, vp]
+        L.bdpt_camera_constants.argtypes = [ctypes.POINTER(_Camera), i32, i32, f32p]
+        L.bdpt_device_count.argtypes = [ctypes.POINTER(i32)]
+        L.bdpt_ctx_create.argtypes = [vp, i32, ctypes.POINTER(vp)]
+        L.bdpt_ctx_destroy.argtypes = [vp]
+        L.bdpt_render.argtypes = [vp, ctypes.POINTER(_FrameParams), vp, vp]
+        L.bdpt_render_host.argtypes = [vp, ctypes.POINTER(_FrameParams), vp]
+        L.bdpt_render_sample.argtypes = [vp, ctypes.POINTER(_FrameParams), f32p, ctypes.c_uint32,
+                                         ctypes.POINTER(i32), f32p, vp]
+        L.bdpt_get_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
+        L.bdpt_synchronize.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise BdptError(f"bdpt error {rc}: {lib().bdpt_last_error().decode()}")
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    _check(lib().bdpt_device_count(ctypes.byref(n)))
+    return n.value
+
+
+@dataclass
+class Camera:
+    eye: tuple = (0.0, 0.8, 3.8)
+    at: tuple = (0.0, 0.8, 0.0)
+    up: tuple = (0.0, 1.0, 0.0)
+    fov: float = 30.0
+
+    def c(self) -> _Camera:
+        c = _Camera()
+        c.eye[:], c.at[:], c.up[:] = list(map(float, self.eye)), list(map(float, self.at)), list(map(float, self.up))
+        c.fov = float(self.fov)
+        return c
+
+
+@dataclass
+class Config:
+    """The subset of the reference's Config (core.h:195-248) the BDPT path reads."""
+    camera: Camera = field(default_factory=Camera)
+    width: int = 768   # main.cpp:41-42 defaults
+    height: int = 576
+    spp: int = 1       # main.cpp:112
+    rr_depth: int = 5  # main.cpp:105
+    rr_prob: float = 0.0  # read but unused: NO_RR = 1 (bdpt.h:18)
+    strategy: int = STRATEGY_BDPT
+    seed_base: int = REFERENCE_SEED
+
+
+@dataclass
+class Ray:
+    o: tuple
+    d: tuple
+    min_t: float = 1e-8
+    max_t: float = 3.402823466e38
+
+
+class Sampler:
+    """std::mt19937(seed) plus the number of floats already drawn."""
+
+    def __init__(self, seed: int):
+        self.seed = int(seed) & 0xFFFFFFFF
+        self.draws = 0
+
+    @staticmethod
+    def for_sample(pixel: int, spp: int, k: int, base: int = REFERENCE_SEED) -> "Sampler":
+        return Sampler((base + pixel * spp + k) & 0xFFFFFFFF)
+
+
+class Scene:
+    def __init__(self, obj_path: str):
+        h = ctypes.c_void_p()
+        _check(lib().bdpt_scene_load_obj(obj_path.encode(), ctypes.byref(h)))
+        self._h = h
+        self.path = obj_path
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.bdpt_scene_free(self._h)
+            self._h = None
+
+    def info(self) -> dict:
+        i = _SceneInfo()
+        _check(lib().bdpt_scene_get_info(self._h, ctypes.byref(i)))
+        return {n: getattr(i, n) for n, _ in _SceneInfo._fields_}
+
+    def export(self):
+        """(tri_f32[n,18], tri_i32[n,3], node_f32[m,6], node_u32[m,3]) in the reference's dump layout."""
+        inf = self.info()
+        n, m = inf["triangles"], inf["bvh_nodes"]
+        tf, ti = np.zeros((n, 18), np.float32), np.zeros((n, 3), np.int32)
+        nf, nu = np.zeros((m, 6), np.float32), np.zeros((m, 3), np.uint32)
+        _check(lib().bdpt_scene_export(self._h, tf.ctypes.data, ti.ctypes.data, nf.ctypes.data, nu.ctypes.data))
+        return tf, ti, nf, nu
+
+
+def camera_constants(cam: Camera, width: int, height: int) -> np.ndarray:
+    out = np.zeros(72, np.float32)
+    c = cam.c()
+    _check(lib().bdpt_camera_constants(ctypes.byref(c), width, height,
+                                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    return out
+
+
+class BDPTIntegrator:
+    """GPU BDPT integrator with the reference's Integrator interface."""
+
+    def __init__(self, scene: Scene, config: Config, device: int = 0):
+        self.scene = scene
+        self.config = config
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(lib().bdpt_ctx_create(scene._h, device, ctypes.byref(h)))
+        self._h = h
+        self.rgb = None
+
+    def close(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.bdpt_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def init(self) -> bool:
+        self.rgb = np.zeros((self.config.height, self.config.width, 3), np.float32)
+        return True
+
+    def params(self, row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> _FrameParams:
+        c = self.config
+        p = _FrameParams()
+        p.camera = c.camera.c()
+        p.width, p.height, p.spp, p.rr_depth = c.width, c.height, c.spp, c.rr_depth
+        p.strategy, p.seed_base = c.strategy, c.seed_base & 0xFFFFFFFF
+        p.row_offset, p.row_stride, p.flags = row_offset, row_stride, flags
+        return p
+
+    def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:
+        """Integrator::render(const Ray&, Sampler&): Li of one camera sample;
+        its light-path splats are added to self.rgb; the sampler advances."""
+        if self.rgb is None:
+            self.init()
+        r = (ctypes.c_float * 8)(*ray.o, *ray.d, ray.min_t, ray.max_t)
+        draws = ctypes.c_int32(sampler.draws)
+        Li = (ctypes.c_float * 3)()
+        p = self.params()
+        _check(lib().bdpt_render_sample(self._h, ctypes.byref(p), r, sampler.seed, ctypes.byref(draws), Li,
+                                        self.rgb.ctypes.data))
+        sampler.draws = draws.value
+        return np.array(Li[:], np.float32)
+
+    def render_frame(self, row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> np.ndarray:
+        """All pixels x spp of the (sharded) image into self.rgb (host copy)."""
+        if self.rgb is None:
+            self.init()
+        p = self.params(row_offset, row_stride, flags)
+        _check(lib().bdpt_render_host(self._h, ctypes.byref(p), self.rgb.ctypes.data))
+        return self.rgb
+
+    def render_device(self, fb_ptr: int, stream_ptr: int = 0, row_offset: int = 0, row_stride: int = 1,
+                      flags: int = 0) -> None:
+        """Asynchronous render into a device framebuffer (e.g. a torch tensor's data_ptr())."""
+        p = self.params(row_offset, row_stride, flags)
+        _check(lib().bdpt_render(self._h, ctypes.byref(p), ctypes.c_void_p(fb_ptr), ctypes.c_void_p(stream_ptr)))
+
+    def stats(self) -> dict:
+        s = _Stats()
+        _check(lib().bdpt_get_stats(self._h, ctypes.byref(s)))
+        return dict(kernel_ms=s.kernel_ms, samples=s.samples, launches=s.launches,
+                    counters=dict(zip(COUNTER_NAMES, list(s.counters))))
+
+    def synchronize(self) -> None:
+        _check(lib().bdpt_synchronize(self._h))

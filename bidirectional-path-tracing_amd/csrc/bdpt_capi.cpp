@@ -1,0 +1,362 @@
+// C-ABI implementation (include/bdpt_amd.h): scene ingest, device context,
+// frame and single-sample renders. Host code only; kernels live in
+// bdpt_kernels.hip. No CPU fallback exists: every render runs the HIP kernels.
+#include "../../include/bdpt_amd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "bdpt_device.hpp"
+#include "scene.hpp"
+
+namespace bdpt {
+hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint32_t nslots,
+                        unsigned long long* work, unsigned long long* counters, int grid, hipStream_t stream);
+hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, const dev::Ray& ray,
+                         uint32_t seed, uint32_t draws, float* out, hipStream_t stream);
+int frame_kernel_stack_depth();
+int frame_kernel_block();
+int light_vertex_fields();
+}  // namespace bdpt
+
+using namespace bdpt;
+
+namespace {
+thread_local std::string g_error;
+
+int fail(int code, const std::string& msg) {
+    g_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                               \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess) return fail(BDPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kMaxRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
+}  // namespace
+
+struct bdpt_scene {
+    HostScene host;
+    DeviceLayout layout;
+};
+
+struct bdpt_ctx {
+    int device = 0;
+    int cus = 0;
+    int grid = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // scene arrays
+    std::vector<void*> allocs;
+    dev::DevScene sc{};
+    int max_depth = 0;
+    int64_t scene_bytes = 0;
+    // work buffers
+    unsigned long long* work = nullptr;      // work counter
+    unsigned long long* counters = nullptr;  // kCounters
+    float* lv = nullptr;
+    size_t lv_floats = 0;
+    uint32_t nslots = 0;
+    float* tmp_fb = nullptr;
+    size_t tmp_fb_floats = 0;
+    float* sample_out = nullptr;
+    // stats of the last render
+    bool pending_timing = false;
+    bdpt_stats stats{};
+};
+
+extern "C" {
+
+const char* bdpt_last_error(void) { return g_error.c_str(); }
+const char* bdpt_version(void) { return "bdpt_amd 0.1 (gfx950 megakernel v0)"; }
+
+int bdpt_scene_load_obj(const char* obj_path, bdpt_scene** out) {
+    if (!obj_path || !out) return fail(BDPT_ERR_INVALID, "null argument");
+    auto s = std::make_unique<bdpt_scene>();
+    std::string err;
+    if (!load_obj_scene(obj_path, s->host, err)) return fail(BDPT_ERR_IO, err);
+    if (!build_device_layout(s->host, s->layout, err)) return fail(BDPT_ERR_INVALID, err);
+    *out = s.release();
+    return BDPT_OK;
+}
+
+int bdpt_scene_free(bdpt_scene* scene) {
+    delete scene;
+    return BDPT_OK;
+}
+
+int bdpt_scene_get_info(const bdpt_scene* s, bdpt_scene_info* out) {
+    if (!s || !out) return fail(BDPT_ERR_INVALID, "null argument");
+    out->triangles = static_cast<int64_t>(s->host.num_triangles());
+    out->bvh_nodes = static_cast<int64_t>(s->host.nodes.size());
+    out->shapes = static_cast<int64_t>(s->host.shape_first.size());
+    out->materials = static_cast<int64_t>(s->host.materials.size());
+    out->emitters = static_cast<int64_t>(s->host.emitters.size());
+    out->bvh_max_depth = s->host.max_depth;
+    const DeviceLayout& L = s->layout;
+    out->device_bytes = static_cast<int64_t>((L.tri.size() + L.shade.size() + L.nodes.size() + L.emit_tri.size()) * 16 +
+                                             L.bsdfs.size() * sizeof(BsdfRecord) +
+                                             L.emitters.size() * sizeof(EmitterRecord) + L.emit_cdf.size() * 4 +
+                                             L.shape_emitter.size() * 4);
+    return BDPT_OK;
+}
+
+int bdpt_scene_export(const bdpt_scene* s, float* tri_f32, int32_t* tri_i32, float* node_f32, uint32_t* node_u32) {
+    if (!s) return fail(BDPT_ERR_INVALID, "null scene");
+    const HostScene& h = s->host;
+    for (size_t i = 0; i < h.num_triangles(); i++) {
+        const size_t t = static_cast<size_t>(h.order[i]);
+        if (tri_f32) {
+            std::memcpy(tri_f32 + 18 * i, &h.pos[9 * t], 9 * sizeof(float));
+            std::memcpy(tri_f32 + 18 * i + 9, &h.nrm[9 * t], 9 * sizeof(float));
+        }
+        if (tri_i32) {
+            tri_i32[3 * i] = h.tri_shape[t];
+            tri_i32[3 * i + 1] = h.tri_prim[t];
+            tri_i32[3 * i + 2] = h.tri_mat[t];
+        }
+    }
+    for (size_t i = 0; i < h.nodes.size(); i++) {
+        if (node_f32) {
+            std::memcpy(node_f32 + 6 * i, h.nodes[i].bmin, 3 * sizeof(float));
+            std::memcpy(node_f32 + 6 * i + 3, h.nodes[i].bmax, 3 * sizeof(float));
+        }
+        if (node_u32) {
+            node_u32[3 * i] = h.nodes[i].start;
+            node_u32[3 * i + 1] = h.nodes[i].nprims;
+            node_u32[3 * i + 2] = h.nodes[i].right_offset;
+        }
+    }
+    return BDPT_OK;
+}
+
+int bdpt_camera_constants(const bdpt_camera* cam, int32_t width, int32_t height, float out[72]) {
+    if (!cam || !out || width <= 0 || height <= 0) return fail(BDPT_ERR_INVALID, "bad camera arguments");
+    CameraConstants c;
+    camera_constants(cam->eye, cam->at, cam->up, cam->fov, width, height, c);
+    std::memcpy(out, &c, sizeof(c));
+    return BDPT_OK;
+}
+
+int bdpt_device_count(int32_t* count) {
+    if (!count) return fail(BDPT_ERR_INVALID, "null argument");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return BDPT_OK;
+}
+
+static int upload(bdpt_ctx* c, const void* src, size_t bytes, void** dst) {
+    if (bytes == 0) bytes = 16;
+    HIP_TRY(hipMalloc(dst, bytes));
+    c->allocs.push_back(*dst);
+    if (src) HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    c->scene_bytes += static_cast<int64_t>(bytes);
+    return BDPT_OK;
+}
+
+int bdpt_ctx_destroy(bdpt_ctx* c) {
+    if (!c) return BDPT_OK;
+    (void)hipSetDevice(c->device);
+    // Teardown is best effort: errors here cannot be acted on by the caller.
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (void* p : c->allocs) (void)hipFree(p);
+    for (void* p : {static_cast<void*>(c->work), static_cast<void*>(c->counters), static_cast<void*>(c->lv),
+                    static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out)})
+        if (p) (void)hipFree(p);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return BDPT_OK;
+}
+
+int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
+    if (!s || !out) return fail(BDPT_ERR_INVALID, "null argument");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(BDPT_ERR_NO_DEVICE, "no HIP device available");
+    if (hip_device < 0 || hip_device >= n) return fail(BDPT_ERR_INVALID, "hip_device out of range");
+    if (s->host.max_depth + 2 > frame_kernel_stack_depth())
+        return fail(BDPT_ERR_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
+    auto c = std::make_unique<bdpt_ctx>();
+    c->device = hip_device;
+    HIP_TRY(hipSetDevice(hip_device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, hip_device));
+    c->cus = prop.multiProcessorCount;
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&c->ev0));
+    HIP_TRY(hipEventCreate(&c->ev1));
+    const DeviceLayout& L = s->layout;
+    void* p;
+    int rc;
+    if ((rc = upload(c.get(), L.tri.data(), L.tri.size() * 16, &p))) return rc;
+    c->sc.tri = static_cast<const float4*>(p);
+    if ((rc = upload(c.get(), L.shade.data(), L.shade.size() * 16, &p))) return rc;
+    c->sc.shade = static_cast<const float4*>(p);
+    if ((rc = upload(c.get(), L.nodes.data(), L.nodes.size() * 16, &p))) return rc;
+    c->sc.nodes = static_cast<const float4*>(p);
+    if ((rc = upload(c.get(), L.bsdfs.data(), L.bsdfs.size() * sizeof(BsdfRecord), &p))) return rc;
+    c->sc.bsdf = static_cast<const BsdfRecord*>(p);
+    if ((rc = upload(c.get(), L.emitters.data(), L.emitters.size() * sizeof(EmitterRecord), &p))) return rc;
+    c->sc.emit = static_cast<const EmitterRecord*>(p);
+    if ((rc = upload(c.get(), L.emit_tri.data(), L.emit_tri.size() * 16, &p))) return rc;
+    c->sc.emit_tri = static_cast<const float4*>(p);
+    if ((rc = upload(c.get(), L.emit_cdf.data(), L.emit_cdf.size() * 4, &p))) return rc;
+    c->sc.emit_cdf = static_cast<const float*>(p);
+    if ((rc = upload(c.get(), L.shape_emitter.data(), L.shape_emitter.size() * 4, &p))) return rc;
+    c->sc.shape_emitter = static_cast<const int32_t*>(p);
+    c->sc.root_link = L.root_link;
+    c->sc.nemit = static_cast<int32_t>(L.emitters.size());
+    c->max_depth = s->host.max_depth;
+    HIP_TRY(hipMalloc(&c->work, sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&c->counters, sizeof(unsigned long long) * BDPT_NUM_COUNTERS));
+    HIP_TRY(hipMalloc(&c->sample_out, 16 * sizeof(float)));
+    // Persistent grid: every CU holds 4 blocks of 256 lanes (LDS stack 40 KiB each).
+    c->grid = c->cus * 4;
+    c->nslots = static_cast<uint32_t>(c->grid * frame_kernel_block());
+    *out = c.release();
+    return BDPT_OK;
+}
+
+static int check_params(const bdpt_frame_params* p) {
+    if (!p) return fail(BDPT_ERR_INVALID, "null params");
+    if (p->width <= 0 || p->height <= 0 || p->spp <= 0) return fail(BDPT_ERR_INVALID, "width/height/spp must be > 0");
+    if (static_cast<int64_t>(p->width) * p->height >= (1ll << 31))
+        return fail(BDPT_ERR_INVALID, "image too large (W*H must fit int32, as in the reference)");
+    if (p->rr_depth < 1 || p->rr_depth > kMaxRrDepth)
+        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth must be in [1, 28] (lazy MT19937 window)");
+    if (p->strategy < 0 || p->strategy > 2) return fail(BDPT_ERR_INVALID, "unknown strategy");
+    if (p->row_stride < 1 || p->row_offset < 0) return fail(BDPT_ERR_INVALID, "bad row shard");
+    return BDPT_OK;
+}
+
+static dev::DevFrame make_frame(const bdpt_frame_params* p) {
+    dev::DevFrame fr{};
+    camera_constants(p->camera.eye, p->camera.at, p->camera.up, p->camera.fov, p->width, p->height, fr.cam);
+    for (int i = 0; i < 3; i++) fr.cam_o[i] = p->camera.eye[i];
+    fr.W = p->width, fr.H = p->height, fr.spp = p->spp, fr.rr_depth = p->rr_depth, fr.strategy = p->strategy;
+    fr.seed_base = p->seed_base;
+    fr.row_offset = p->row_offset, fr.row_stride = p->row_stride;
+    fr.nrows = p->row_offset >= p->height ? 0 : (p->height - p->row_offset + p->row_stride - 1) / p->row_stride;
+    fr.flags = p->flags;
+    fr.total_samples = static_cast<uint64_t>(fr.nrows) * static_cast<uint64_t>(p->width) * p->spp;
+    return fr;
+}
+
+static int ensure_lv(bdpt_ctx* c, int rr_depth, uint32_t nslots) {
+    const size_t need = static_cast<size_t>(std::max(rr_depth - 1, 1)) * light_vertex_fields() * nslots;
+    if (need > c->lv_floats) {
+        if (c->lv) HIP_TRY(hipFree(c->lv));
+        c->lv = nullptr;
+        HIP_TRY(hipMalloc(&c->lv, need * sizeof(float)));
+        c->lv_floats = need;
+    }
+    return BDPT_OK;
+}
+
+int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_stream) {
+    if (!c || !fb) return fail(BDPT_ERR_INVALID, "null argument");
+    int rc = check_params(p);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    if ((rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
+    const dev::DevFrame fr = make_frame(p);
+    HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
+    HIP_TRY(hipEventRecord(c->ev0, st));
+    if (fr.total_samples > 0)
+        HIP_TRY(launch_frame(c->sc, fr, fb, c->lv, c->nslots, c->work, c->counters, c->grid, st));
+    HIP_TRY(hipEventRecord(c->ev1, st));
+    c->pending_timing = true;
+    c->stats = bdpt_stats{};
+    c->stats.samples = static_cast<int64_t>(fr.total_samples);
+    c->stats.launches = fr.total_samples > 0 ? 1 : 0;
+    return BDPT_OK;
+}
+
+int bdpt_get_stats(bdpt_ctx* c, bdpt_stats* out) {
+    if (!c || !out) return fail(BDPT_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->pending_timing) {
+        HIP_TRY(hipEventSynchronize(c->ev1));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->stats.kernel_ms = ms;
+        unsigned long long host[BDPT_NUM_COUNTERS];
+        HIP_TRY(hipMemcpy(host, c->counters, sizeof(host), hipMemcpyDeviceToHost));
+        for (int i = 0; i < BDPT_NUM_COUNTERS; i++) c->stats.counters[i] = static_cast<int64_t>(host[i]);
+        c->pending_timing = false;
+    }
+    *out = c->stats;
+    return BDPT_OK;
+}
+
+int bdpt_synchronize(bdpt_ctx* c) {
+    if (!c) return fail(BDPT_ERR_INVALID, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    return BDPT_OK;
+}
+
+static int ensure_tmp_fb(bdpt_ctx* c, size_t floats) {
+    if (floats > c->tmp_fb_floats) {
+        if (c->tmp_fb) HIP_TRY(hipFree(c->tmp_fb));
+        c->tmp_fb = nullptr;
+        HIP_TRY(hipMalloc(&c->tmp_fb, floats * sizeof(float)));
+        c->tmp_fb_floats = floats;
+    }
+    return BDPT_OK;
+}
+
+int bdpt_render_host(bdpt_ctx* c, const bdpt_frame_params* p, float* fb_host) {
+    if (!c || !fb_host) return fail(BDPT_ERR_INVALID, "null argument");
+    int rc = check_params(p);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = static_cast<size_t>(p->width) * p->height * 3;
+    if ((rc = ensure_tmp_fb(c, n))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->tmp_fb, fb_host, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if ((rc = bdpt_render(c, p, c->tmp_fb, c->stream))) return rc;
+    HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_render_sample(bdpt_ctx* c, const bdpt_frame_params* p, const float ray[8], uint32_t seed,
+                       int32_t* draws, float Li[3], float* fb_host) {
+    if (!c || !ray || !draws || !Li || !fb_host) return fail(BDPT_ERR_INVALID, "null argument");
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (*draws < 0 || *draws + 10 + 8 * (p->rr_depth - 1) > 226)
+        return fail(BDPT_ERR_UNSUPPORTED, "sampler advanced beyond the lazy MT19937 window");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = static_cast<size_t>(p->width) * p->height * 3;
+    if ((rc = ensure_tmp_fb(c, n))) return rc;
+    if ((rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->tmp_fb, fb_host, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    const dev::DevFrame fr = make_frame(p);
+    dev::Ray r{dev::f3{ray[0], ray[1], ray[2]}, dev::f3{ray[3], ray[4], ray[5]}, ray[6], ray[7]};
+    HIP_TRY(launch_sample(c->sc, fr, c->tmp_fb, c->lv, r, seed, static_cast<uint32_t>(*draws), c->sample_out, c->stream));
+    float out[4];
+    HIP_TRY(hipMemcpyAsync(out, c->sample_out, sizeof(out), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    Li[0] = out[0], Li[1] = out[1], Li[2] = out[2];
+    uint32_t used;
+    std::memcpy(&used, &out[3], 4);
+    *draws = static_cast<int32_t>(used);
+    return BDPT_OK;
+}
+
+}  // extern "C"

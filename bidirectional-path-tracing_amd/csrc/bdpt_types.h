@@ -1,0 +1,63 @@
+// Plain-old-data records shared by the host ingest and the HIP kernels.
+//
+// HBM layout (all arrays 16-byte aligned, read through float4 loads):
+//   tri[3*i + c]   c=0..2: (v_c.x, v_c.y, v_c.z, 0)          triangle i in BVH leaf order
+//   shade[3*i + c] c=0..2: (n_c.x, n_c.y, n_c.z, id_c)       id_0 = matID, id_1 = shapeID,
+//                                                            id_2 = primID (int bits)
+//   nodes[4*j + q] interior node j (2-wide, both child boxes inline):
+//       q0 = c0.min.xyz, c0.max.x   q1 = c0.max.yz, c1.min.xy
+//       q2 = c1.min.z, c1.max.xyz   q3 = (link0, link1, 0, 0) as uint bits
+//     link: bit 31 set -> leaf, start = (link >> 3) & 0x0fffffff, count = link & 7
+//           otherwise  -> index of the child's interior record
+//   emit_tri[5*f + q] emitter faces in shape face order (v0 v1 v2 n0 n1 n2 packed)
+#pragma once
+
+#include <cstdint>
+
+namespace bdpt {
+
+struct alignas(16) float4_t {
+    float x, y, z, w;
+};
+
+enum BsdfKind : int32_t {
+    BSDF_NULL = 0,     // illum 5: the reference leaves a null BSDF (renderer.cpp:268)
+    BSDF_DIFFUSE = 1,  // illum 7: src/bsdfs/diffuse.h
+    BSDF_MIRROR = 2,   // illum 3: src/bsdfs/perfectmirror.h
+    BSDF_GLASS = 3,    // illum 6: src/bsdfs/glass.h
+    BSDF_MIXTURE = 4,  // illum 8: src/bsdfs/mixture.h
+    BSDF_PHONG = 5,    // any other illum: src/bsdfs/phong.h
+};
+
+// BSDF::EBSDFType bits (reference src/core/core.h:261-295).
+constexpr uint32_t kTypeNull = 0x1u, kTypeDiffuseRefl = 0x2u, kTypeGlossyRefl = 0x8u, kTypeDeltaRefl = 0x20u,
+                   kTypeDeltaTrans = 0x40u;
+constexpr uint32_t kTypeDelta = kTypeNull | kTypeDeltaRefl | kTypeDeltaTrans;
+
+struct BsdfRecord {
+    int32_t kind;
+    uint32_t type;
+    float kd[3], ks[3], tf[3], emission[3];
+    float exponent, ior, scale, specw;
+};
+
+struct EmitterRecord {
+    int32_t shape;
+    int32_t nfaces;
+    int32_t face_offset;  // into emit_tri (faces)
+    int32_t cdf_offset;   // into emit_cdf (nfaces + 1 entries)
+    float area;
+    float radiance[3];
+};
+
+struct CameraConstants {
+    float w2c[16], c2w[16], c2clip[16], ndc2screen[16];  // column-major (glm)
+    float invW, invH, angle, aspect;
+    float fwd[3];
+    float vnear;
+};
+
+constexpr uint32_t kLeafBit = 0x80000000u;
+inline uint32_t make_leaf_link(uint32_t start, uint32_t count) { return kLeafBit | (start << 3) | count; }
+
+}  // namespace bdpt

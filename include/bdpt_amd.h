@@ -1,0 +1,135 @@
+/*
+ * bdpt_amd — MI355X-native bidirectional path tracer: the C-ABI drop-in
+ * boundary for the reference's BDPT hot path.
+ *
+ * Reference (JackMinn/Bidirectional-Path-Tracing) interfaces these entry points
+ * replace:
+ *   bdpt_scene_load_obj      Scene::load                      src/core/renderer.cpp:235-315
+ *                            (tinyobj LoadObj :249, BSDFs per illum :258-271,
+ *                             emitters :279-305, AcceleratorBVH::build accel.h:115-123)
+ *   bdpt_camera_constants    camera set-up of Renderer::render renderer.cpp:140-153
+ *                            and BDPTIntegrator bdpt.h:49-54, :485-489
+ *   bdpt_ctx_create          Integrator::init (rgb allocation) src/core/integrator.cpp:16-20
+ *                            + upload of the Scene the integrator holds by reference
+ *   bdpt_render              the offline loop of Renderer::render renderer.cpp:130-214
+ *                            calling BDPTIntegrator::render bdpt.h:219-241 for every
+ *                            (pixel, sample), with camera splats (bdpt.h:295-371)
+ *                            accumulated into the same framebuffer
+ *   bdpt_render_sample       virtual v3f Integrator::render(const Ray&, Sampler&) const
+ *                            src/core/integrator.h:48, overridden at bdpt.h:219
+ *   bdpt_ctx_destroy         Integrator/Renderer teardown (renderer.cpp:221-227)
+ *
+ * Conventions: plain C types only; status 0 = OK, < 0 = error (message from
+ * bdpt_last_error(), thread-local). A context is bound to one HIP device and is
+ * not thread-safe. Nothing here falls back to the CPU: without a HIP device,
+ * bdpt_ctx_create fails with BDPT_ERR_NO_DEVICE.
+ *
+ * Determinism: camera sample (pixel p, sample k) draws from
+ * std::mt19937(seed_base + p*spp + k) exactly like the reference's Sampler
+ * (src/core/math.h:63-76), and all arithmetic follows the reference's single-
+ * precision operation order, so paths are identical to the CPU reference; only
+ * the order of floating-point additions into the framebuffer differs.
+ */
+#ifndef BDPT_AMD_H
+#define BDPT_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BDPT_OK 0
+#define BDPT_ERR_INVALID -1
+#define BDPT_ERR_IO -2
+#define BDPT_ERR_NO_DEVICE -3
+#define BDPT_ERR_HIP -4
+#define BDPT_ERR_UNSUPPORTED -5
+
+/* Strategy switches of the reference (bdpt.h:16-17, compile-time there). */
+#define BDPT_STRATEGY_BDPT 0
+#define BDPT_STRATEGY_LIGHT_TRACING 1
+#define BDPT_STRATEGY_PATH_TRACING 2
+
+/* bdpt_frame_params.flags */
+#define BDPT_FLAG_COUNT 1u            /* counting pass: fill bdpt_stats.counters (slower) */
+#define BDPT_FLAG_FULL_TRAVERSAL 2u   /* visit every box the reference visits (no t-culling) */
+
+typedef struct bdpt_scene bdpt_scene; /* host-side ingested scene */
+typedef struct bdpt_ctx bdpt_ctx;     /* device context (one HIP device) */
+
+typedef struct {
+    int64_t triangles, bvh_nodes, shapes, materials, emitters, bvh_max_depth;
+    int64_t device_bytes; /* HBM bytes of the uploaded scene arrays */
+} bdpt_scene_info;
+
+typedef struct {
+    float eye[3], at[3], up[3]; /* [camera] eye / at / up (main.cpp:31-37) */
+    float fov;                  /* degrees */
+} bdpt_camera;
+
+typedef struct {
+    bdpt_camera camera;
+    int32_t width, height; /* [film] (the global image; shards still splat into it) */
+    int32_t spp;           /* [renderer] spp */
+    int32_t rr_depth;      /* [renderer] rrDepth: hard path-depth cap (NO_RR=1, bdpt.h:18) */
+    int32_t strategy;      /* BDPT_STRATEGY_* (reference default: BDPT) */
+    uint32_t seed_base;    /* 260450963 = the reference's Sampler seed (renderer.cpp:155) */
+    int32_t row_offset;    /* shard: render rows row_offset, row_offset+row_stride, ... */
+    int32_t row_stride;    /*        (1 = whole image)                                   */
+    uint32_t flags;        /* BDPT_FLAG_* */
+} bdpt_frame_params;
+
+#define BDPT_NUM_COUNTERS 8
+/* counters: [0] closest-hit rays, [1] shadow rays, [2] interior-node visits,
+ * [3] triangle tests, [4] light vertices stored, [5] light-vertex reads,
+ * [6] camera splats, [7] RNG draws. */
+typedef struct {
+    double kernel_ms;      /* HIP-event time of the render kernel(s) of the last call */
+    int64_t samples;       /* camera samples rendered by the last call */
+    int64_t launches;      /* kernel launches of the last call */
+    int64_t counters[BDPT_NUM_COUNTERS];
+} bdpt_stats;
+
+const char* bdpt_last_error(void);
+const char* bdpt_version(void);
+
+/* ---- host-side scene ingest (no GPU needed) ---- */
+int bdpt_scene_load_obj(const char* obj_path, bdpt_scene** out);
+int bdpt_scene_free(bdpt_scene* scene);
+int bdpt_scene_get_info(const bdpt_scene* scene, bdpt_scene_info* out);
+/* Reference-layout export (tests): tri_f32[ntri][18] = v0 v1 v2 n0 n1 n2 in BVH
+ * leaf order, tri_i32[ntri][3] = shapeID primID matID, node_f32[nnodes][6] =
+ * bbox min/max, node_u32[nnodes][3] = start nPrims rightOffset (flat preorder). */
+int bdpt_scene_export(const bdpt_scene* scene, float* tri_f32, int32_t* tri_i32, float* node_f32, uint32_t* node_u32);
+/* Camera constants: worldToCamera, cameraToWorld, cameraToClip, NDCToScreen
+ * (column-major) then invWidth, invHeight, tan(fov/2), aspect, forward.xyz,
+ * virtual near-plane distance — 72 floats. */
+int bdpt_camera_constants(const bdpt_camera* cam, int32_t width, int32_t height, float out[72]);
+
+/* ---- device ---- */
+int bdpt_device_count(int32_t* count);
+int bdpt_ctx_create(const bdpt_scene* scene, int32_t hip_device, bdpt_ctx** out);
+int bdpt_ctx_destroy(bdpt_ctx* ctx);
+
+/* Renders every (pixel, sample) of the shard and ADDS the result to fb_device
+ * (device pointer, width*height*3 floats, pixel-major RGB, row 0 = top): eye
+ * estimates acc/spp per pixel plus every light-path camera splat (which may land
+ * on rows outside the shard). Asynchronous on `hip_stream` (hipStream_t; NULL =
+ * the context's own stream); timing is read with bdpt_get_stats after a sync. */
+int bdpt_render(bdpt_ctx* ctx, const bdpt_frame_params* params, float* fb_device, void* hip_stream);
+/* Same, with a host framebuffer (copied to the device, accumulated, copied back). Synchronous. */
+int bdpt_render_host(bdpt_ctx* ctx, const bdpt_frame_params* params, float* fb_host);
+/* One camera sample through BDPTIntegrator::render(ray, sampler): ray = o.xyz d.xyz
+ * min_t max_t; the sampler is std::mt19937(sampler_seed) after *sampler_draws
+ * draws (updated on return). Returns Li; splats are added to fb_host. Synchronous. */
+int bdpt_render_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, const float ray[8], uint32_t sampler_seed,
+                       int32_t* sampler_draws, float Li[3], float* fb_host);
+int bdpt_get_stats(bdpt_ctx* ctx, bdpt_stats* out);
+/* Waits for all work queued by this context (on every stream it was given). */
+int bdpt_synchronize(bdpt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
