@@ -17,10 +17,13 @@
 
 namespace bdpt {
 hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint32_t nslots,
-                        unsigned long long* work, unsigned long long* counters, int grid, hipStream_t stream);
+                        unsigned long long* work, unsigned long long* counters, int grid, hipStream_t stream,
+                        void* dparams);
+size_t frame_params_bytes();
 hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, const dev::Ray& ray,
                          uint32_t seed, uint32_t draws, float* out, hipStream_t stream);
 int frame_kernel_stack_depth();
+int frame_kernel_blocks_per_cu();
 int frame_kernel_block();
 int light_vertex_fields();
 }  // namespace bdpt
@@ -69,6 +72,7 @@ struct bdpt_ctx {
     float* tmp_fb = nullptr;
     size_t tmp_fb_floats = 0;
     float* sample_out = nullptr;
+    void* dparams = nullptr;  // kernel parameter block (filled in stream order per launch)
     // stats of the last render
     bool pending_timing = false;
     bdpt_stats stats{};
@@ -171,7 +175,7 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocs) (void)hipFree(p);
     for (void* p : {static_cast<void*>(c->work), static_cast<void*>(c->counters), static_cast<void*>(c->lv),
-                    static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out)})
+                    static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -221,8 +225,10 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     HIP_TRY(hipMalloc(&c->work, sizeof(unsigned long long)));
     HIP_TRY(hipMalloc(&c->counters, sizeof(unsigned long long) * BDPT_NUM_COUNTERS));
     HIP_TRY(hipMalloc(&c->sample_out, 16 * sizeof(float)));
-    // Persistent grid: every CU holds 4 blocks of 256 lanes (LDS stack 40 KiB each).
-    c->grid = c->cus * 4;
+    HIP_TRY(hipMalloc(&c->dparams, frame_params_bytes()));
+    // Persistent grid: exactly the resident blocks (no co-residency is assumed:
+    // the work queue has no inter-block waits, extra blocks would just queue).
+    c->grid = c->cus * frame_kernel_blocks_per_cu();
     c->nslots = static_cast<uint32_t>(c->grid * frame_kernel_block());
     *out = c.release();
     return BDPT_OK;
@@ -276,7 +282,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
     if (fr.total_samples > 0)
-        HIP_TRY(launch_frame(c->sc, fr, fb, c->lv, c->nslots, c->work, c->counters, c->grid, st));
+        HIP_TRY(launch_frame(c->sc, fr, fb, c->lv, c->nslots, c->work, c->counters, c->grid, st, c->dparams));
     HIP_TRY(hipEventRecord(c->ev1, st));
     c->pending_timing = true;
     c->stats = bdpt_stats{};

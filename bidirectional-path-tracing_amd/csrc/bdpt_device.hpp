@@ -205,6 +205,46 @@ __device__ __forceinline__ bool slab(float lx, float ly, float lz, float hx, flo
     return true;
 }
 
+// Fast form of the same decision: t = (l - o) * RN(1/d) differs from the
+// reference's RN((l - o) / d) by at most ~1.8e-7 |t| (three roundings). With
+// per-axis intervals [lo_i, hi_i], the reference's test is "every cross pair
+// lo_i <= hi_j (i != j) holds" (the swaps make lo_i <= hi_i). Each cross pair is
+// decided with a slack of 1e-6 (|lo_i| + |hi_j|) — 5x the error bound — and any
+// pair inside the slack, or any non-finite value, defers to slab() above, so
+// the hit / miss outcome is always the reference's.
+enum : int { kSlabMiss = 0, kSlabHit = 1, kSlabAmbiguous = 2 };
+__device__ __forceinline__ int cross_le(float a, float b) {
+    const float d = b - a, s = 1e-6f * (fabsf(a) + fabsf(b));
+    return d > s ? kSlabHit : (d < -s ? kSlabMiss : kSlabAmbiguous);
+}
+__device__ __forceinline__ int slab_fast(float lx, float ly, float lz, float hx, float hy, float hz, f3 o, f3 inv,
+                                         float& tn, float& tf) {
+    const float x0 = (lx - o.x) * inv.x, x1 = (hx - o.x) * inv.x;
+    const float y0 = (ly - o.y) * inv.y, y1 = (hy - o.y) * inv.y;
+    const float z0 = (lz - o.z) * inv.z, z1 = (hz - o.z) * inv.z;
+    const float nan_probe = ((x0 + x1) + (y0 + y1)) + (z0 + z1);  // NaN if any t is NaN (or +inf meets -inf)
+    if (nan_probe != nan_probe) return kSlabAmbiguous;           // the reference's NaN rules live in slab()
+    const float lox = fminf(x0, x1), hix = fmaxf(x0, x1);
+    const float loy = fminf(y0, y1), hiy = fmaxf(y0, y1);
+    const float loz = fminf(z0, z1), hiz = fmaxf(z0, z1);
+    tn = fmaxf(fmaxf(lox, loy), loz);
+    tf = fminf(fminf(hix, hiy), hiz);
+    const int c1 = cross_le(loy, hix), c2 = cross_le(loz, hix), c3 = cross_le(lox, hiy);
+    const int c4 = cross_le(lox, hiz), c5 = cross_le(loy, hiz), c6 = cross_le(loz, hiy);
+    if (c1 == kSlabMiss || c2 == kSlabMiss || c3 == kSlabMiss || c4 == kSlabMiss || c5 == kSlabMiss ||
+        c6 == kSlabMiss)
+        return kSlabMiss;
+    if ((c1 & c2 & c3 & c4 & c5 & c6) == kSlabHit) return kSlabHit;
+    return kSlabAmbiguous;  // includes NaN / inf operands (every comparison false)
+}
+
+__device__ __forceinline__ bool box_test(float lx, float ly, float lz, float hx, float hy, float hz, const Ray& r,
+                                         f3 inv, float& tn, float& tf) {
+    const int f = slab_fast(lx, ly, lz, hx, hy, hz, r.o, inv, tn, tf);
+    if (f != kSlabAmbiguous) return f == kSlabHit;
+    return slab(lx, ly, lz, hx, hy, hz, r, tn, tf);
+}
+
 // rayTriangleIntersect (core.h:379-400) + accel.h:43's t > 1e-3.
 __device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_t i, const Ray& r, float& t, float& u,
                                          float& v) {
@@ -261,6 +301,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool a
     if (r.min_t > best_t) return -1;  // the root's entry mint is min_t (bvh.h:277, :287)
     uint32_t link = sc.root_link;
     int sp = 0;
+    const f3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
     for (;;) {
         if (link & kLeafBit) {
             const uint32_t start = (link >> 3) & 0x0fffffffu, count = link & 7u;
@@ -287,8 +328,8 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool a
             const float4* nd = sc.nodes + 4 * static_cast<size_t>(link);
             const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
             float tn0, tf0, tn1, tf1;
-            bool h0 = slab(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, r, tn0, tf0);
-            bool h1 = slab(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r, tn1, tf1);
+            bool h0 = box_test(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, r, inv, tn0, tf0);
+            bool h1 = box_test(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r, inv, tn1, tf1);
             const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
             if (!FULL) {
                 const float far = cull_far(any ? r.max_t : best_t);
@@ -338,20 +379,24 @@ __device__ __forceinline__ Ray shadow_ray(f3 start, f3 end) {
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 
 // MixtureBSDF::eval == PhongBSDF::eval (mixture.h:59-75, phong.h:56-71).
+// With Ks == 0 the specular term is (0 * (n + 2)) * INV_TWOPI * powf(c, n) = +0
+// (powf of c in [0, 1] is finite), and val + 0 == val: skipping it is exact.
 __device__ __forceinline__ f3 glossy_eval(const BsdfRecord& b, f3 wi, f3 wo) {
     f3 val = mk(0.f, 0.f, 0.f);
     if (wi.z >= 0.f && wo.z >= 0.f) {
         val = val + ld3(b.kd) * kInvPi;
-        const float ex = b.exponent;
-        const float c = glibc_fminf(glibc_fmaxf(dot(wi, reflect_z(wo)), 0.f), 1.f);
-        val = val + ((ld3(b.ks) * (ex + 2)) * kInvTwoPi) * glibc_powf(c, ex);
+        if (b.ks[0] != 0.f || b.ks[1] != 0.f || b.ks[2] != 0.f) {
+            const float ex = b.exponent;
+            const float c = glibc_fminf(glibc_fmaxf(dot(wi, reflect_z(wo)), 0.f), 1.f);
+            val = val + ((ld3(b.ks) * (ex + 2)) * kInvTwoPi) * glibc_powf(c, ex);
+        }
         val = val * b.scale;
         val = val * wi.z;
     }
     return val;
 }
 
-__device__ __forceinline__ f3 bsdf_eval(const BsdfRecord& b, f3 wi, f3 wo) {
+__device__ BDPT_NOINLINE f3 bsdf_eval(const BsdfRecord& b, f3 wi, f3 wo) {
     if (b.kind == BSDF_DIFFUSE) {  // diffuse.h:35-43
         if (wi.z >= 0.f && wo.z >= 0.f) return (ld3(b.kd) * kInvPi) * wi.z;
         return mk(0.f, 0.f, 0.f);
@@ -367,11 +412,14 @@ __device__ __forceinline__ float phong_part_pdf(const BsdfRecord& b, f3 wi, f3 w
     return phong_lobe_pdf(to_local(rs, rt, rn, wi), b.exponent);
 }
 
-__device__ __forceinline__ float bsdf_pdf(const BsdfRecord& b, f3 wi, f3 wo) {
+// With specw == 0, pdfPhong * 0 = +0 (pdfPhong is finite and >= 0) and
+// 0 + pdfDiffuse * (1 - 0) == pdfDiffuse: skipping the Phong lobe is exact.
+__device__ BDPT_NOINLINE float bsdf_pdf(const BsdfRecord& b, f3 wi, f3 wo) {
     if (b.kind == BSDF_DIFFUSE) return cosine_hemisphere_pdf(wi);  // diffuse.h:45-50
     if (b.kind == BSDF_MIXTURE) {                                  // mixture.h:78-100
-        const float pp = phong_part_pdf(b, wi, wo);
         const float pd = cosine_hemisphere_pdf(wi);
+        if (b.specw == 0.f) return pd;
+        const float pp = phong_part_pdf(b, wi, wo);
         return (pp * b.specw) + (pd * (1.f - b.specw));
     }
     if (b.kind == BSDF_PHONG) return phong_part_pdf(b, wi, wo);  // phong.h:73-83
@@ -389,7 +437,7 @@ __device__ __forceinline__ float fresnel_dielectric(float eta_i, float eta_t, fl
 }
 
 // BSDF::sample: sets wi, returns f*cos, writes the solid-angle pdf.
-__device__ __forceinline__ f3 bsdf_sample(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
+__device__ BDPT_NOINLINE f3 bsdf_sample(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
     switch (b.kind) {
         case BSDF_DIFFUSE:  // diffuse.h:52-61
             wi = cosine_hemisphere(u);

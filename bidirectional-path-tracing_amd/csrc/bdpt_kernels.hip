@@ -25,6 +25,9 @@
 namespace bdpt {
 namespace dev {
 
+#ifndef BDPT_WAVES_PER_EU
+#define BDPT_WAVES_PER_EU 3  // waves per SIMD the register allocator must leave room for
+#endif
 constexpr int kBlock = 256;
 constexpr int kStackDepth = 40;  // >= max BVH depth + 1 (checked on the host)
 constexpr int kLvFields = 16;    // p.xyz n.xyz wo.xyz tp.xyz vcm vc rr mat
@@ -509,21 +512,37 @@ __device__ __forceinline__ void flush_counts(const Counts& cnt, unsigned long lo
     }
 }
 
+// Kernel parameters live in a small device buffer; the loop re-derives its
+// pointer to them every iteration (through an empty asm) so the compiler loads
+// the rarely used camera / frame constants at their point of use instead of
+// pinning ~100 of them in SGPRs for the whole persistent loop (which spilled).
+struct KParams {
+    DevScene sc;
+    DevFrame fr;
+    float* fb;
+    float* lv;
+    uint32_t nslots;
+    unsigned long long* work;
+    unsigned long long* counters;
+};
+
 template <bool FULL, bool COUNT>
-__global__ __launch_bounds__(kBlock, 4) void bdpt_frame_kernel(DevScene sc, DevFrame fr, float* __restrict__ fb,
-                                                            float* __restrict__ lvbuf, uint32_t nslots,
-                                                            unsigned long long* __restrict__ work,
-                                                            unsigned long long* __restrict__ counters) {
+__global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(const KParams* __restrict__ kpp) {
+    const KParams& kp = *kpp;
     __shared__ uint32_t stack_mem[kStackDepth * kBlock];
     const int lane = threadIdx.x & 63;
     const Stack stk{stack_mem + threadIdx.x, kBlock};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
-    const LightStore ls{lvbuf, nslots, blockIdx.x * kBlock + threadIdx.x};
+    const LightStore ls{kp.lv, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
+    unsigned long long* const work = kp.work;
+    const uint64_t total = kp.fr.total_samples;
     Lane L;
     L.state = ST_IDLE;
     bool exhausted = false;  // wave-uniform
     for (;;) {
+        const KParams* P = kpp;
+        asm volatile("" : "+s"(P));
         if (!exhausted) {  // refill idle lanes: one atomic per wave
             const uint64_t idle = __ballot(L.state == ST_IDLE);
             if (idle) {
@@ -534,18 +553,18 @@ __global__ __launch_bounds__(kBlock, 4) void bdpt_frame_kernel(DevScene sc, DevF
                 base = __shfl(base, leader);
                 if (L.state == ST_IDLE) {
                     const uint64_t s = base + __popcll(idle & ((1ull << lane) - 1ull));
-                    if (s < fr.total_samples) start_sample(L, s, fr);
+                    if (s < total) start_sample(L, s, P->fr);
                 }
-                if (base + n >= fr.total_samples) exhausted = true;
+                if (base + n >= total) exhausted = true;
             }
         }
         if (__ballot(L.state != ST_IDLE) == 0) {
             if (exhausted) break;
             continue;
         }
-        if (L.state != ST_IDLE) step<FULL, COUNT>(L, sc, fr, fb, ls, stk, cnt);
+        if (L.state != ST_IDLE) step<FULL, COUNT>(L, P->sc, P->fr, P->fb, ls, stk, cnt);
     }
-    if (COUNT) flush_counts(cnt, counters);
+    if (COUNT) flush_counts(cnt, kp.counters);
 }
 
 // One Integrator::render(ray, sampler) call on one lane. out = Li.xyz, draws.
@@ -574,21 +593,23 @@ __global__ __launch_bounds__(64) void bdpt_sample_kernel(DevScene sc, DevFrame f
 }  // namespace dev
 
 // ------------------------------------------------------------ host launchers
+size_t frame_params_bytes() { return sizeof(dev::KParams); }
+
+// `dparams` is a device buffer of frame_params_bytes() owned by the caller; it
+// is filled on `stream` before the launch (stream order protects reuse).
 hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint32_t nslots,
-                        unsigned long long* work, unsigned long long* counters, int grid, hipStream_t stream) {
+                        unsigned long long* work, unsigned long long* counters, int grid, hipStream_t stream,
+                        void* dparams) {
     const bool full = (fr.flags & 2u) != 0, count = (fr.flags & 1u) != 0;
-    if (full && count)
-        hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, true>), dim3(grid), dim3(dev::kBlock), 0, stream, sc, fr, fb,
-                           lvbuf, nslots, work, counters);
-    else if (full)
-        hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, false>), dim3(grid), dim3(dev::kBlock), 0, stream, sc, fr, fb,
-                           lvbuf, nslots, work, counters);
-    else if (count)
-        hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, true>), dim3(grid), dim3(dev::kBlock), 0, stream, sc, fr, fb,
-                           lvbuf, nslots, work, counters);
-    else
-        hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, false>), dim3(grid), dim3(dev::kBlock), 0, stream, sc, fr,
-                           fb, lvbuf, nslots, work, counters);
+    const dev::KParams host{sc, fr, fb, lvbuf, nslots, work, counters};
+    hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    const dev::KParams* kp = static_cast<const dev::KParams*>(dparams);
+    const dim3 g(grid), b(dev::kBlock);
+    if (full && count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, true>), g, b, 0, stream, kp);
+    else if (full) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, false>), g, b, 0, stream, kp);
+    else if (count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, true>), g, b, 0, stream, kp);
+    else hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, false>), g, b, 0, stream, kp);
     return hipGetLastError();
 }
 
@@ -596,6 +617,16 @@ hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float
                          uint32_t seed, uint32_t draws, float* out, hipStream_t stream) {
     hipLaunchKernelGGL(dev::bdpt_sample_kernel, dim3(1), dim3(64), 0, stream, sc, fr, fb, lvbuf, ray, seed, draws, out);
     return hipGetLastError();
+}
+
+// Resident 256-lane blocks per CU for the frame kernel (VGPR and LDS limited).
+int frame_kernel_blocks_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::bdpt_frame_kernel<false, false>, dev::kBlock, 0) !=
+            hipSuccess ||
+        n <= 0)
+        n = BDPT_WAVES_PER_EU;
+    return n;
 }
 
 int frame_kernel_stack_depth() { return dev::kStackDepth; }

@@ -21,6 +21,10 @@
 namespace bdpt {
 namespace dev {
 
+// Large, rarely-divergent helpers are real calls: one copy of their code in the
+// megakernel instead of one per call site (i-cache and register pressure).
+#define BDPT_NOINLINE __attribute__((noinline))
+
 // ---------------------------------------------------------------- float3
 struct f3 {
     float x, y, z;
@@ -137,7 +141,7 @@ __device__ __noinline__ double sincos_reduce_large(uint32_t xi, int* np) {
 }
 
 // which = 0: sinf, 1: cosf
-__device__ __forceinline__ float glibc_sincosf(float y, int which) {
+__device__ BDPT_NOINLINE float glibc_sincosf(float y, int which) {
     double x = y;
     if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
         double x2 = x * x;
@@ -260,7 +264,7 @@ __device__ __noinline__ float powf_special(float x, float y, uint32_t ix, uint32
     return 0.f;
 }
 
-__device__ __forceinline__ float glibc_powf(float x, float y) {
+__device__ BDPT_NOINLINE float glibc_powf(float x, float y) {
     uint32_t sign_bias = 0;
     uint32_t ix = f2u(x), iy = f2u(y);
     if (ix - 0x00800000 >= 0x7f800000 - 0x00800000 || powf_zeroinfnan(iy)) {
