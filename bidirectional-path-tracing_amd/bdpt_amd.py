@@ -31,7 +31,8 @@ STRATEGY_BDPT, STRATEGY_LIGHT_TRACING, STRATEGY_PATH_TRACING = 0, 1, 2
 FLAG_COUNT, FLAG_FULL_TRAVERSAL = 1, 2
 REFERENCE_SEED = 260450963  # renderer.cpp:155
 COUNTER_NAMES = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
-                 "light_vert_reads", "splats", "rng_draws"]
+                 "light_vert_reads", "splats", "rng_draws", "trav_lane_iters", "trav_wave_iters",
+                 "shade_lane_actions", "shade_wave_actions"]
 
 
 class BdptError(RuntimeError):
@@ -56,7 +57,7 @@ class _SceneInfo(ctypes.Structure):
 
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
-                ("counters", ctypes.c_int64 * 8)]
+                ("counters", ctypes.c_int64 * 12)]
 
 
 def build(force: bool = False) -> str:

@@ -17,7 +17,7 @@ constexpr float kInvPi = 0.31830988618379067154f;     // platform.h:51
 constexpr float kInvTwoPi = 0.15915494309189533577f;  // platform.h:52
 constexpr float kEpsilon = 1e-8f;                     // platform.h:56
 constexpr float kTriMinT = 0x1.0624dep-10f;           // smallest float t with (double)t > 1e-3 (accel.h:43)
-constexpr int kCounters = 8;
+constexpr int kCounters = 12;
 
 // ------------------------------------------------------------------ inputs
 struct DevScene {
@@ -286,6 +286,11 @@ struct Counts {
     uint32_t c[kCounters];
 };
 
+// SIMD-efficiency probe: true on the lowest active lane of the wave only.
+__device__ __forceinline__ bool first_active_lane() {
+    return (__lane_id()) == static_cast<unsigned>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1);
+}
+
 // BVH::getIntersection (bvh.h:259-352) for both query kinds, in ONE inlined
 // loop so the megakernel carries a single copy of the traversal:
 //   closest (any == false): the minimum-t triangle, ties to the lowest leaf
@@ -303,6 +308,10 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool a
     int sp = 0;
     const f3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
     for (;;) {
+        if (COUNT) {
+            cnt.c[8]++;
+            if (first_active_lane()) cnt.c[9]++;
+        }
         if (link & kLeafBit) {
             const uint32_t start = (link >> 3) & 0x0fffffffu, count = link & 7u;
             bool done = false;

@@ -215,6 +215,12 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
     const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
     const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
     while (act != A_ISSUED && act != A_DONE) {
+        if (COUNT) {
+            cnt.c[10]++;
+            // one wave-level execution per distinct action present among active lanes
+            for (uint32_t a = A_START_LIGHT; a <= A_FINISH; a++)
+                if (__ballot(act == a) && act == a && first_active_lane()) cnt.c[11]++;
+        }
         switch (act) {
             case A_START_LIGHT: {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
                 float emitterPdf, areaPdf;

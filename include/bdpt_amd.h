@@ -80,10 +80,12 @@ typedef struct {
     uint32_t flags;        /* BDPT_FLAG_* */
 } bdpt_frame_params;
 
-#define BDPT_NUM_COUNTERS 8
+#define BDPT_NUM_COUNTERS 12
 /* counters: [0] closest-hit rays, [1] shadow rays, [2] interior-node visits,
  * [3] triangle tests, [4] light vertices stored, [5] light-vertex reads,
- * [6] camera splats, [7] RNG draws. */
+ * [6] camera splats, [7] RNG draws; SIMD-efficiency probes: [8] traversal
+ * iterations summed over lanes, [9] the same counted once per wave, [10]
+ * state-machine actions summed over lanes, [11] action executions per wave. */
 typedef struct {
     double kernel_ms;      /* HIP-event time of the render kernel(s) of the last call */
     int64_t samples;       /* camera samples rendered by the last call */

@@ -1,0 +1,28 @@
+"""Counting-pass probe: per-sample work counts and SIMD-efficiency ratios of
+the frame kernel (python tools/probe.py [scene] [W] [H] [spp])."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "bidirectional-path-tracing_amd"), os.path.join(REPO, "scenes")]
+import bdpt_amd  # noqa: E402
+import variants  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "caustic"
+W, H, spp = (int(x) for x in (sys.argv[2:5] if len(sys.argv) > 4 else (512, 512, 4)))
+sc = variants.SCENES[name]
+cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**sc["camera"]), width=W, height=H, spp=spp, rr_depth=sc["rr_depth"])
+it = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(name)), cfg)
+it.init()
+it.render_frame()
+t_plain = it.stats()["kernel_ms"]
+it.render_frame(flags=bdpt_amd.FLAG_COUNT)
+st = it.stats()
+c, n = st["counters"], st["samples"]
+out = {k: round(v / n, 3) for k, v in c.items()}
+out["trav_simd_eff"] = round(c["trav_lane_iters"] / max(64 * c["trav_wave_iters"], 1), 4)
+out["shade_simd_eff"] = round(c["shade_lane_actions"] / max(64 * c["shade_wave_actions"], 1), 4)
+out["kernel_ms"] = round(t_plain, 3)
+out["msamples_per_s"] = round(n / t_plain * 1e-3, 3)
+print(json.dumps({"scene": name, "W": W, "H": H, "spp": spp, **out}))
