@@ -25,14 +25,16 @@ from dataclasses import dataclass, field
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libbdpt_amd.so")
+# BDPT_AMD_LIB selects an alternative in-tree build (kernel-variant experiments).
+LIB_PATH = os.environ.get("BDPT_AMD_LIB") or os.path.join(HERE, "lib", "libbdpt_amd.so")
 
 STRATEGY_BDPT, STRATEGY_LIGHT_TRACING, STRATEGY_PATH_TRACING = 0, 1, 2
 FLAG_COUNT, FLAG_FULL_TRAVERSAL = 1, 2
 REFERENCE_SEED = 260450963  # renderer.cpp:155
 COUNTER_NAMES = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
                  "light_vert_reads", "splats", "rng_draws", "trav_lane_iters", "trav_wave_iters",
-                 "shade_lane_actions", "shade_wave_actions"]
+                 "shade_lane_actions", "shade_wave_actions", "trav_clocks", "shade_clocks", "loop_clocks",
+                 "slab_fallbacks"]
 
 
 class BdptError(RuntimeError):
@@ -52,12 +54,13 @@ class _FrameParams(ctypes.Structure):
 
 class _SceneInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in
-                ("triangles", "bvh_nodes", "shapes", "materials", "emitters", "bvh_max_depth", "device_bytes")]
+                ("triangles", "bvh_nodes", "shapes", "materials", "emitters", "bvh_max_depth", "device_bytes",
+                 "bvh_leaves", "wide_nodes", "wide_depth", "wide_max_stack")]
 
 
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
-                ("counters", ctypes.c_int64 * 12)]
+                ("counters", ctypes.c_int64 * 16)]
 
 
 def build(force: bool = False) -> str:

@@ -16,13 +16,13 @@
 #include "scene.hpp"
 
 namespace bdpt {
-hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint32_t nslots,
-                        unsigned long long* work, unsigned long long* counters, int grid, hipStream_t stream,
-                        void* dparams);
+hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                        uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
+                        hipStream_t stream, void* dparams);
 size_t frame_params_bytes();
-hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, const dev::Ray& ray,
-                         uint32_t seed, uint32_t draws, float* out, hipStream_t stream);
-int frame_kernel_stack_depth();
+hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                         const dev::Ray& ray, uint32_t seed, uint32_t draws, float* out, hipStream_t stream);
+int frame_kernel_lds_stack();
 int frame_kernel_blocks_per_cu();
 int frame_kernel_block();
 int light_vertex_fields();
@@ -68,6 +68,7 @@ struct bdpt_ctx {
     unsigned long long* counters = nullptr;  // kCounters
     float* lv = nullptr;
     size_t lv_floats = 0;
+    uint2* gstack = nullptr;  // traversal-stack overflow beyond the LDS part
     uint32_t nslots = 0;
     float* tmp_fb = nullptr;
     size_t tmp_fb_floats = 0;
@@ -107,7 +108,14 @@ int bdpt_scene_get_info(const bdpt_scene* s, bdpt_scene_info* out) {
     out->emitters = static_cast<int64_t>(s->host.emitters.size());
     out->bvh_max_depth = s->host.max_depth;
     const DeviceLayout& L = s->layout;
-    out->device_bytes = static_cast<int64_t>((L.tri.size() + L.shade.size() + L.nodes.size() + L.emit_tri.size()) * 16 +
+    int64_t leaves = 0;
+    for (const FlatNode& n : s->host.nodes) leaves += (n.right_offset == 0);
+    out->bvh_leaves = leaves;
+    out->wide_nodes = static_cast<int64_t>(L.wnodes.size() / 8);
+    out->wide_depth = L.wdepth;
+    out->wide_max_stack = L.wmax_stack;
+    out->device_bytes = static_cast<int64_t>((L.tri.size() + L.shade.size() + L.nodes.size() + L.wnodes.size() +
+                                              L.emit_tri.size()) * 16 +
                                              L.bsdfs.size() * sizeof(BsdfRecord) +
                                              L.emitters.size() * sizeof(EmitterRecord) + L.emit_cdf.size() * 4 +
                                              L.shape_emitter.size() * 4);
@@ -175,6 +183,7 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocs) (void)hipFree(p);
     for (void* p : {static_cast<void*>(c->work), static_cast<void*>(c->counters), static_cast<void*>(c->lv),
+                    static_cast<void*>(c->gstack),
                     static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -189,8 +198,6 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(BDPT_ERR_NO_DEVICE, "no HIP device available");
     if (hip_device < 0 || hip_device >= n) return fail(BDPT_ERR_INVALID, "hip_device out of range");
-    if (s->host.max_depth + 2 > frame_kernel_stack_depth())
-        return fail(BDPT_ERR_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
     auto c = std::make_unique<bdpt_ctx>();
     c->device = hip_device;
     HIP_TRY(hipSetDevice(hip_device));
@@ -209,6 +216,9 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     c->sc.shade = static_cast<const float4*>(p);
     if ((rc = upload(c.get(), L.nodes.data(), L.nodes.size() * 16, &p))) return rc;
     c->sc.nodes = static_cast<const float4*>(p);
+    if ((rc = upload(c.get(), L.wnodes.data(), L.wnodes.size() * 16, &p))) return rc;
+    c->sc.wnodes = static_cast<const float4*>(p);
+    c->sc.wroot_link = L.wroot_link;
     if ((rc = upload(c.get(), L.bsdfs.data(), L.bsdfs.size() * sizeof(BsdfRecord), &p))) return rc;
     c->sc.bsdf = static_cast<const BsdfRecord*>(p);
     if ((rc = upload(c.get(), L.emitters.data(), L.emitters.size() * sizeof(EmitterRecord), &p))) return rc;
@@ -230,6 +240,12 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     // the work queue has no inter-block waits, extra blocks would just queue).
     c->grid = c->cus * frame_kernel_blocks_per_cu();
     c->nslots = static_cast<uint32_t>(c->grid * frame_kernel_block());
+    // Traversal stack: worst case of either tree (binary: depth + 1 pending
+    // right children; 4-wide: the host-computed bound), the part beyond the
+    // kernel's LDS entries in HBM.
+    const int depth = std::max(s->host.max_depth + 2, L.wmax_stack + 1);
+    const int spill = std::max(0, depth - frame_kernel_lds_stack());
+    HIP_TRY(hipMalloc(&c->gstack, sizeof(uint2) * std::max<size_t>(1, static_cast<size_t>(spill) * c->nslots)));
     *out = c.release();
     return BDPT_OK;
 }
@@ -282,7 +298,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
     if (fr.total_samples > 0)
-        HIP_TRY(launch_frame(c->sc, fr, fb, c->lv, c->nslots, c->work, c->counters, c->grid, st, c->dparams));
+        HIP_TRY(launch_frame(c->sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st, c->dparams));
     HIP_TRY(hipEventRecord(c->ev1, st));
     c->pending_timing = true;
     c->stats = bdpt_stats{};
@@ -353,7 +369,7 @@ int bdpt_render_sample(bdpt_ctx* c, const bdpt_frame_params* p, const float ray[
     HIP_TRY(hipMemcpyAsync(c->tmp_fb, fb_host, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
     const dev::DevFrame fr = make_frame(p);
     dev::Ray r{dev::f3{ray[0], ray[1], ray[2]}, dev::f3{ray[3], ray[4], ray[5]}, ray[6], ray[7]};
-    HIP_TRY(launch_sample(c->sc, fr, c->tmp_fb, c->lv, r, seed, static_cast<uint32_t>(*draws), c->sample_out, c->stream));
+    HIP_TRY(launch_sample(c->sc, fr, c->tmp_fb, c->lv, c->gstack, r, seed, static_cast<uint32_t>(*draws), c->sample_out, c->stream));
     float out[4];
     HIP_TRY(hipMemcpyAsync(out, c->sample_out, sizeof(out), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));

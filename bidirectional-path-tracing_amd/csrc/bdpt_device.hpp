@@ -17,19 +17,31 @@ constexpr float kInvPi = 0.31830988618379067154f;     // platform.h:51
 constexpr float kInvTwoPi = 0.15915494309189533577f;  // platform.h:52
 constexpr float kEpsilon = 1e-8f;                     // platform.h:56
 constexpr float kTriMinT = 0x1.0624dep-10f;           // smallest float t with (double)t > 1e-3 (accel.h:43)
-constexpr int kCounters = 12;
+constexpr int kCounters = 16;
 
 // ------------------------------------------------------------------ inputs
+// Loads through an address-space-1 pointer compile to global_load (SGPR/VGPR
+// addressing, vmcnt only) instead of flat_load: the scene pointers arrive via
+// a parameter block, so the compiler cannot infer their address space itself.
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 gld4(const float4* p) {
+    const v4f_t v = *(const __attribute__((address_space(1))) v4f_t*)(p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float gld1(const float* p) { return *(const __attribute__((address_space(1))) float*)(p); }
+__device__ __forceinline__ void gst1(float* p, float x) { *(__attribute__((address_space(1))) float*)(p) = x; }
+
 struct DevScene {
     const float4* __restrict__ tri;
     const float4* __restrict__ shade;
-    const float4* __restrict__ nodes;
+    const float4* __restrict__ nodes;   // the reference's binary tree (2 child boxes per record)
+    const float4* __restrict__ wnodes;  // 4-wide nodes over the same leaves (wide_bvh.hpp)
     const BsdfRecord* __restrict__ bsdf;
     const EmitterRecord* __restrict__ emit;
     const float4* __restrict__ emit_tri;
     const float* __restrict__ emit_cdf;
     const int32_t* __restrict__ shape_emitter;
-    uint32_t root_link;
+    uint32_t root_link, wroot_link;
     int32_t nemit;
 };
 
@@ -127,7 +139,8 @@ __device__ __forceinline__ f3 uniform_hemisphere(F2 u) {
     float phi = u.x * kPi * 2.0f;
     float cosTheta = u.y;
     float sinTheta = sqrt_cr(glibc_fmaxf(1.f - (cosTheta * cosTheta), 0.f));
-    return mk(sinTheta * glibc_cosf(phi), sinTheta * glibc_sinf(phi), cosTheta);
+    const SinCos sc = glibc_sincosf2(phi);
+    return mk(sinTheta * sc.c, sinTheta * sc.s, cosTheta);
 }
 // squareToUniformDiskConcentric + squareToCosineHemisphere (math.h:153-192)
 __device__ __forceinline__ f3 cosine_hemisphere(F2 u) {
@@ -143,8 +156,9 @@ __device__ __forceinline__ f3 cosine_hemisphere(F2 u) {
             radius = ry;
             phi = (kPi * 0.5f) - ((kPi * 0.25f) * (rx * (1.f / ry)));
         }
-        dx = radius * glibc_cosf(phi);
-        dy = radius * glibc_sinf(phi);
+        const SinCos sc = glibc_sincosf2(phi);
+        dx = radius * sc.c;
+        dy = radius * sc.s;
     }
     float z = 1.0f - (dx * dx + dy * dy);
     z = glibc_fmaxf(z, 0.f);
@@ -156,7 +170,8 @@ __device__ __forceinline__ f3 phong_lobe(F2 u, float ex) {
     float cosTheta = glibc_powf(u.x, 1.f / (ex + 2));
     float sinTheta = sqrt_cr(glibc_fmaxf(1.f - (cosTheta * cosTheta), 0.f));
     float phi = u.y * 2.f * kPi;
-    return mk(sinTheta * glibc_cosf(phi), sinTheta * glibc_sinf(phi), cosTheta);
+    const SinCos sc = glibc_sincosf2(phi);
+    return mk(sinTheta * sc.c, sinTheta * sc.s, cosTheta);
 }
 __device__ __forceinline__ float phong_lobe_pdf(f3 v, float ex) {
     return v.z >= 0.f ? (ex + 2) * kInvTwoPi * glibc_powf(v.z, ex) : 0.f;
@@ -205,51 +220,75 @@ __device__ __forceinline__ bool slab(float lx, float ly, float lz, float hx, flo
     return true;
 }
 
-// Fast form of the same decision: t = (l - o) * RN(1/d) differs from the
-// reference's RN((l - o) / d) by at most ~1.8e-7 |t| (three roundings). With
-// per-axis intervals [lo_i, hi_i], the reference's test is "every cross pair
-// lo_i <= hi_j (i != j) holds" (the swaps make lo_i <= hi_i). Each cross pair is
-// decided with a slack of 1e-6 (|lo_i| + |hi_j|) — 5x the error bound — and any
-// pair inside the slack, or any non-finite value, defers to slab() above, so
-// the hit / miss outcome is always the reference's.
+// Fast form of the same decision. The reference's test (after its swaps every
+// per-axis interval is [lo_i, hi_i]) hits exactly when max_i lo_i <= min_j hi_j.
+// Here t = (l - o) * RN(1/d) differs from the reference's RN((l - o) / d) by at
+// most ~1.8e-7 |t| (three roundings instead of one), so tf - tn differs from the
+// reference's by < 3e-7 (|tn| + |tf|). Decisions within a slack of
+// 1e-6 (|tn| + |tf|) + 1e-30 of the boundary defer to slab() above, so the
+// hit / miss outcome is always the reference's. Rays whose reciprocal
+// direction or origin is not finite (where 0 * inf = NaN could arise) take
+// slab() for every box (RayInv::fast == false).
 enum : int { kSlabMiss = 0, kSlabHit = 1, kSlabAmbiguous = 2 };
-__device__ __forceinline__ int cross_le(float a, float b) {
-    const float d = b - a, s = 1e-6f * (fabsf(a) + fabsf(b));
-    return d > s ? kSlabHit : (d < -s ? kSlabMiss : kSlabAmbiguous);
+struct RayInv {
+    f3 inv;
+    bool fast;
+};
+__device__ __forceinline__ RayInv ray_inv(const Ray& r) {
+    RayInv ri;
+    ri.inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+    const float probe = (ri.inv.x + ri.inv.y + ri.inv.z) * 0.f + ((r.o.x + r.o.y + r.o.z) * 0.f);
+    ri.fast = (probe == 0.f);  // false iff some component is +-inf or NaN
+    return ri;
 }
 __device__ __forceinline__ int slab_fast(float lx, float ly, float lz, float hx, float hy, float hz, f3 o, f3 inv,
                                          float& tn, float& tf) {
     const float x0 = (lx - o.x) * inv.x, x1 = (hx - o.x) * inv.x;
     const float y0 = (ly - o.y) * inv.y, y1 = (hy - o.y) * inv.y;
     const float z0 = (lz - o.z) * inv.z, z1 = (hz - o.z) * inv.z;
-    const float nan_probe = ((x0 + x1) + (y0 + y1)) + (z0 + z1);  // NaN if any t is NaN (or +inf meets -inf)
-    if (nan_probe != nan_probe) return kSlabAmbiguous;           // the reference's NaN rules live in slab()
+    tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    const float d = tf - tn, s = fmaf(fabsf(tn) + fabsf(tf), 1e-6f, 1e-30f);
+    return d > s ? kSlabHit : (d < -s ? kSlabMiss : kSlabAmbiguous);  // inf operands: ambiguous
+}
+
+__device__ __forceinline__ int cross_le(float a, float b) {  // a <= b with the same slack
+    const float d = b - a, s = fmaf(fabsf(a) + fabsf(b), 1e-6f, 1e-30f);
+    return d > s ? kSlabHit : (d < -s ? kSlabMiss : kSlabAmbiguous);
+}
+// Second chance for an ambiguous max-lo vs min-hi decision: the reference's
+// test is the six cross pairs lo_i <= hi_j (i != j) — the pair of a flat
+// (zero-thickness) box axis, tn == tf on a planar wall, never enters it.
+__device__ __forceinline__ int slab_cross(float lx, float ly, float lz, float hx, float hy, float hz, f3 o,
+                                          f3 inv) {
+    const float x0 = (lx - o.x) * inv.x, x1 = (hx - o.x) * inv.x;
+    const float y0 = (ly - o.y) * inv.y, y1 = (hy - o.y) * inv.y;
+    const float z0 = (lz - o.z) * inv.z, z1 = (hz - o.z) * inv.z;
     const float lox = fminf(x0, x1), hix = fmaxf(x0, x1);
     const float loy = fminf(y0, y1), hiy = fmaxf(y0, y1);
     const float loz = fminf(z0, z1), hiz = fmaxf(z0, z1);
-    tn = fmaxf(fmaxf(lox, loy), loz);
-    tf = fminf(fminf(hix, hiy), hiz);
-    const int c1 = cross_le(loy, hix), c2 = cross_le(loz, hix), c3 = cross_le(lox, hiy);
-    const int c4 = cross_le(lox, hiz), c5 = cross_le(loy, hiz), c6 = cross_le(loz, hiy);
-    if (c1 == kSlabMiss || c2 == kSlabMiss || c3 == kSlabMiss || c4 == kSlabMiss || c5 == kSlabMiss ||
-        c6 == kSlabMiss)
-        return kSlabMiss;
-    if ((c1 & c2 & c3 & c4 & c5 & c6) == kSlabHit) return kSlabHit;
-    return kSlabAmbiguous;  // includes NaN / inf operands (every comparison false)
+    const int a = cross_le(lox, fminf(hiy, hiz)), b = cross_le(loy, fminf(hix, hiz)),
+              c = cross_le(loz, fminf(hix, hiy));
+    if (a == kSlabMiss || b == kSlabMiss || c == kSlabMiss) return kSlabMiss;
+    return (a & b & c) == kSlabHit ? kSlabHit : kSlabAmbiguous;
 }
 
+template <bool COUNT>
 __device__ __forceinline__ bool box_test(float lx, float ly, float lz, float hx, float hy, float hz, const Ray& r,
-                                         f3 inv, float& tn, float& tf) {
-    const int f = slab_fast(lx, ly, lz, hx, hy, hz, r.o, inv, tn, tf);
-    if (f != kSlabAmbiguous) return f == kSlabHit;
+                                         const RayInv& ri, float& tn, float& tf, uint32_t& fallbacks) {
+    if (ri.fast) {
+        int f = slab_fast(lx, ly, lz, hx, hy, hz, r.o, ri.inv, tn, tf);
+        if (f == kSlabAmbiguous) f = slab_cross(lx, ly, lz, hx, hy, hz, r.o, ri.inv);
+        if (f != kSlabAmbiguous) return f == kSlabHit;
+    }
+    if (COUNT) fallbacks++;
     return slab(lx, ly, lz, hx, hy, hz, r, tn, tf);
 }
 
 // rayTriangleIntersect (core.h:379-400) + accel.h:43's t > 1e-3.
 __device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_t i, const Ray& r, float& t, float& u,
                                          float& v) {
-    const f3 v0 = xyz(tri[3 * i]), v1 = xyz(tri[3 * i + 1]), v2 = xyz(tri[3 * i + 2]);
-    const f3 e1 = v1 - v0, e2 = v2 - v0;
+    const f3 v0 = xyz(gld4(tri + 3 * i)), e1 = xyz(gld4(tri + 3 * i + 1)), e2 = xyz(gld4(tri + 3 * i + 2));
     const f3 pvec = cross(r.d, e2);
     const float det = dot(e1, pvec);
     if (fabsf(det) < kEpsilon) return false;
@@ -264,19 +303,31 @@ __device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_
     return t >= kTriMinT;
 }
 
-// Traversal stack: one column per thread in LDS (entry k of thread x at
-// base[k * stride + x], conflict-free); entries are node links. 40 entries x
-// 4 B x 1024 threads fill the 160 KiB of a CU at 16 waves.
+// Traversal stack of (link, t_near) entries: the first kLdsStack entries of a
+// lane live in LDS (entry k of thread x at lds[k * stride + x]: 8-byte lanes,
+// conflict-free), deeper ones spill to a per-lane HBM column (rare; the host
+// sizes it to the scene's worst case).
+constexpr int kLdsStack = 16;
+constexpr uint32_t kEmptyLinkDev = 0xffffffffu;  // unused 4-wide child slot
 struct Stack {
-    uint32_t* base;
+    uint2* lds;
     int stride;
-    __device__ __forceinline__ void put(int k, uint32_t link) { base[k * stride] = link; }
-    __device__ __forceinline__ uint32_t get(int k) const { return base[k * stride]; }
+    uint2* gbl;  // entry k >= kLdsStack at gbl[(k - kLdsStack) * nslots + slot]
+    uint32_t nslots, slot;
+    __device__ __forceinline__ void put(int k, uint32_t link, float tn) const {
+        const uint2 e = make_uint2(link, __float_as_uint(tn));
+        if (k < kLdsStack) lds[k * stride] = e;
+        else gbl[static_cast<size_t>(k - kLdsStack) * nslots + slot] = e;
+    }
+    __device__ __forceinline__ uint2 get(int k) const {
+        if (k < kLdsStack) return lds[k * stride];
+        return gbl[static_cast<size_t>(k - kLdsStack) * nslots + slot];
+    }
 };
 
 // Conservative distance culling. The reference never culls by distance
 // (bbhits stay 0, bvh.h:265-337): its result is the minimum-t triangle among
-// ALL boxes the line crosses, first-found (= lowest leaf index) on ties. Boxes
+// ALL reachable leaves, first-found (= lowest leaf index) on ties. Boxes
 // entered beyond best + margin, or exited before t = 5e-4, cannot hold a
 // triangle that changes that result.
 __device__ __forceinline__ float cull_far(float best) { return best + fabsf(best) * 1e-3f + 1e-4f; }
@@ -291,71 +342,172 @@ __device__ __forceinline__ bool first_active_lane() {
     return (__lane_id()) == static_cast<unsigned>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1);
 }
 
-// BVH::getIntersection (bvh.h:259-352) for both query kinds, in ONE inlined
-// loop so the megakernel carries a single copy of the traversal:
-//   closest (any == false): the minimum-t triangle, ties to the lowest leaf
-//     index (= first found by the reference's left-first DFS); returns the leaf
-//     index or -1 and the hit's t, u, v.
-//   any (any == true): returns 1 if some triangle hits inside [min_t, max_t]
-//     (the occlusion early-out at bvh.h:300-302), else -1.
-template <bool FULL, bool COUNT>
-__device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool any, Stack stk, float& bt, float& bu,
-                                        float& bv, Counts& cnt) {
-    float best_t = r.max_t, best_u = 0.f, best_v = 0.f;
-    int best = -1;
-    if (r.min_t > best_t) return -1;  // the root's entry mint is min_t (bvh.h:277, :287)
+// Triangle tests of one reference leaf (bvh.h:291-309). Closest: keeps the
+// minimum t, ties to the lowest index (the reference's strict `<` in its
+// left-first DFS = leaf order). Any: true on a hit inside [min_t, max_t].
+template <bool COUNT>
+__device__ __forceinline__ bool leaf_tests(const DevScene& sc, uint32_t link, const Ray& r, bool any, float& best_t,
+                                           int& best, float& best_u, float& best_v, uint32_t& tri_count) {
+    const uint32_t start = (link >> 3) & 0x0fffffffu, count = link & 7u;
+    for (uint32_t k = 0; k < count; k++) {
+        const uint32_t i = start + k;
+        float t, u, v;
+        if (COUNT) tri_count++;
+        if (tri_test(sc.tri, i, r, t, u, v)) {
+            if (any) {
+                if (t <= r.max_t && t >= r.min_t) {
+                    best = 1;
+                    return true;
+                }
+            } else if (t < best_t || (t == best_t && best >= 0 && static_cast<int>(i) < best)) {
+                best_t = t, best = static_cast<int>(i), best_u = u, best_v = v;
+            }
+        }
+    }
+    return false;
+}
+
+struct TravResult {
+    int best;
+    float t, u, v;
+    uint32_t nodes, tris, exact;  // counting pass only
+};
+
+// BVH::getIntersection (bvh.h:259-352) over the reference's own binary tree:
+// every box decided exactly as the reference decides it. Used for rays the
+// 4-wide hierarchy cannot serve (zero / non-finite reciprocal direction, where
+// the slab test is not monotone) and for BDPT_FLAG_FULL_TRAVERSAL (cull =
+// false: every box the reference visits). Out of line, arguments by value
+// (nothing of the caller's lives in scratch).
+template <bool COUNT>
+__device__ BDPT_NOINLINE TravResult traverse_binary(const DevScene& sc, Ray r, bool any, bool cull, Stack stk) {
+    TravResult res{-1, r.max_t, 0.f, 0.f, 0u, 0u, 0u};
     uint32_t link = sc.root_link;
     int sp = 0;
-    const f3 inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
     for (;;) {
-        if (COUNT) {
-            cnt.c[8]++;
-            if (first_active_lane()) cnt.c[9]++;
-        }
         if (link & kLeafBit) {
-            const uint32_t start = (link >> 3) & 0x0fffffffu, count = link & 7u;
-            bool done = false;
-            for (uint32_t k = 0; k < count; k++) {
-                const uint32_t i = start + k;
-                float t, u, v;
-                if (COUNT) cnt.c[3]++;
-                if (tri_test(sc.tri, i, r, t, u, v)) {
-                    if (any) {
-                        if (t <= r.max_t && t >= r.min_t) {
-                            best = 1;
-                            done = true;
-                            break;
-                        }
-                    } else if (t < best_t || (t == best_t && best >= 0 && static_cast<int>(i) < best)) {
-                        best_t = t, best = static_cast<int>(i), best_u = u, best_v = v;
-                    }
-                }
-            }
-            if (done) break;
+            if (leaf_tests<COUNT>(sc, link, r, any, res.t, res.best, res.u, res.v, res.tris)) break;
         } else {
-            if (COUNT) cnt.c[2]++;
+            if (COUNT) res.nodes++, res.exact += 2;
             const float4* nd = sc.nodes + 4 * static_cast<size_t>(link);
-            const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+            const float4 q0 = gld4(nd), q1 = gld4(nd + 1), q2 = gld4(nd + 2), q3 = gld4(nd + 3);
             float tn0, tf0, tn1, tf1;
-            bool h0 = box_test(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, r, inv, tn0, tf0);
-            bool h1 = box_test(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r, inv, tn1, tf1);
+            bool h0 = slab(q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, r, tn0, tf0);
+            bool h1 = slab(q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r, tn1, tf1);
             const uint32_t l0 = __float_as_uint(q3.x), l1 = __float_as_uint(q3.y);
-            if (!FULL) {
-                const float far = cull_far(any ? r.max_t : best_t);
+            if (cull) {
+                const float far = cull_far(any ? r.max_t : res.t);
                 h0 = h0 && !(tn0 > far) && !(tf0 < kCullNear);
                 h1 = h1 && !(tn1 > far) && !(tf1 < kCullNear);
             }
             if (h0 && h1) {
-                const bool swap = !FULL && (tn1 < tn0);
-                stk.put(sp++, swap ? l0 : l1);
-                link = swap ? l1 : l0;
+                stk.put(sp++, l1, 0.f);
+                link = l0;
                 continue;
             }
             if (h0) { link = l0; continue; }
             if (h1) { link = l1; continue; }
         }
         if (sp == 0) break;
-        link = stk.get(--sp);
+        link = stk.get(--sp).x;
+    }
+    return res;
+}
+
+// Fast, conservative box decision for one child of a 4-wide node: the slab
+// intervals from RN(1/d), then tn/tf and the max-lo <= min-hi decision with the
+// slack of slab_fast (kSlabAmbiguous when too close to call).
+__device__ __forceinline__ int child_fast(float lx, float hx, float ly, float hy, float lz, float hz, f3 o, f3 inv,
+                                          float& tn, float& tf) {
+    return slab_fast(lx, ly, lz, hx, hy, hz, o, inv, tn, tf);
+}
+
+// Closest-hit / occlusion query over the 4-wide hierarchy (wide_bvh.hpp).
+// Interior children: a conservative test (ambiguous counts as a hit) — any box
+// containing a reachable leaf box passes the reference's test, so it is never
+// rejected. Leaf children (the reference's leaves): decided exactly (fast
+// test, then the cross pairs, then the reference's own divisions). Children
+// are visited near-first; stacked entries carry their entry distance and are
+// dropped on pop once a closer hit exists.
+template <bool FULL, bool COUNT>
+__device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool any, const Stack& stk, float& bt,
+                                        float& bu, float& bv, Counts& cnt) {
+    if (r.min_t > r.max_t) return -1;  // the root's entry mint is min_t (bvh.h:277, :287)
+    const RayInv ri = ray_inv(r);
+    if (FULL || !ri.fast) {
+        const TravResult q = traverse_binary<COUNT>(sc, r, any, !FULL, stk);
+        if (COUNT) cnt.c[2] += q.nodes, cnt.c[3] += q.tris, cnt.c[15] += q.exact;
+        bt = q.t, bu = q.u, bv = q.v;
+        return q.best;
+    }
+    float best_t = r.max_t, best_u = 0.f, best_v = 0.f;
+    int best = -1;
+    uint32_t link = sc.wroot_link;
+    int sp = 0;
+    for (;;) {
+        if (COUNT) {
+            cnt.c[8]++;
+            if (first_active_lane()) cnt.c[9]++;
+        }
+        if (link & kLeafBit) {
+            if (leaf_tests<COUNT>(sc, link, r, any, best_t, best, best_u, best_v, cnt.c[3])) break;
+        } else {
+            if (COUNT) cnt.c[2]++;
+            const float4* nd = sc.wnodes + 8 * static_cast<size_t>(link);
+            const float4 lx = gld4(nd), hx = gld4(nd + 1), ly = gld4(nd + 2), hy = gld4(nd + 3), lz = gld4(nd + 4),
+                         hz = gld4(nd + 5), lk = gld4(nd + 6);
+            const float far = cull_far(any ? r.max_t : best_t);
+            float key[4];
+            uint32_t lnk[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const float clx = (&lx.x)[c], chx = (&hx.x)[c], cly = (&ly.x)[c], chy = (&hy.x)[c],
+                            clz = (&lz.x)[c], chz = (&hz.x)[c];
+                const uint32_t l = __float_as_uint((&lk.x)[c]);
+                float tn, tf;
+                int d = child_fast(clx, chx, cly, chy, clz, chz, r.o, ri.inv, tn, tf);
+                const bool leaf = (l & kLeafBit) != 0 && l != kEmptyLinkDev;
+                if (d == kSlabAmbiguous && leaf) {
+                    d = slab_cross(clx, cly, clz, chx, chy, chz, r.o, ri.inv);
+                    if (d == kSlabAmbiguous) {
+                        if (COUNT) cnt.c[15]++;
+                        float en, ex;
+                        d = slab(clx, cly, clz, chx, chy, chz, r, en, ex) ? kSlabHit : kSlabMiss;
+                    }
+                }
+                const bool hit = l != kEmptyLinkDev && d != kSlabMiss && !(tn > far) && !(tf < kCullNear);
+                key[c] = hit ? tn : __builtin_inff();
+                lnk[c] = hit ? l : kEmptyLinkDev;
+            }
+            // near-first order: sorting network on (key, link)
+#define BDPT_CE(a, b)                                                   \
+    {                                                                   \
+        const bool sw = key[b] < key[a];                                \
+        const float k0 = sw ? key[b] : key[a], k1 = sw ? key[a] : key[b]; \
+        const uint32_t l0 = sw ? lnk[b] : lnk[a], l1 = sw ? lnk[a] : lnk[b]; \
+        key[a] = k0, key[b] = k1, lnk[a] = l0, lnk[b] = l1;             \
+    }
+            BDPT_CE(0, 1) BDPT_CE(2, 3) BDPT_CE(0, 2) BDPT_CE(1, 3) BDPT_CE(1, 2)
+#undef BDPT_CE
+            if (lnk[0] != kEmptyLinkDev) {
+                if (lnk[3] != kEmptyLinkDev) stk.put(sp++, lnk[3], key[3]);
+                if (lnk[2] != kEmptyLinkDev) stk.put(sp++, lnk[2], key[2]);
+                if (lnk[1] != kEmptyLinkDev) stk.put(sp++, lnk[1], key[1]);
+                link = lnk[0];
+                continue;
+            }
+        }
+        // pop the nearest pending entry that can still hold a closer hit
+        bool found = false;
+        while (sp > 0) {
+            const uint2 e = stk.get(--sp);
+            if (!(__uint_as_float(e.y) > cull_far(any ? r.max_t : best_t))) {
+                link = e.x;
+                found = true;
+                break;
+            }
+        }
+        if (!found) break;
     }
     bt = best_t, bu = best_u, bv = best_v;
     return best;
@@ -363,8 +515,9 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool a
 
 // AcceleratorBVH::intersect's shading of a closest hit (accel.h:133-166).
 __device__ __forceinline__ void shade_hit(const DevScene& sc, int i, float u, float v, float t, f3 dir, Hit& h) {
-    const f3 v0 = xyz(sc.tri[3 * i]), v1 = xyz(sc.tri[3 * i + 1]), v2 = xyz(sc.tri[3 * i + 2]);
-    const float4 s0 = sc.shade[3 * i], s1 = sc.shade[3 * i + 1], s2 = sc.shade[3 * i + 2];
+    const float4* sh = sc.shade + 5 * static_cast<size_t>(i);
+    const f3 v0 = xyz(gld4(sc.tri + 3 * i)), v1 = xyz(gld4(sh + 3)), v2 = xyz(gld4(sh + 4));
+    const float4 s0 = gld4(sh), s1 = gld4(sh + 1), s2 = gld4(sh + 2);
     const float w = 1 - u - v;
     h.p = (v0 * w + v1 * u) + v2 * v;
     h.n = normalize((xyz(s0) * w + xyz(s1) * u) + xyz(s2) * v);
@@ -405,12 +558,17 @@ __device__ __forceinline__ f3 glossy_eval(const BsdfRecord& b, f3 wi, f3 wo) {
     return val;
 }
 
-__device__ BDPT_NOINLINE f3 bsdf_eval(const BsdfRecord& b, f3 wi, f3 wo) {
-    if (b.kind == BSDF_DIFFUSE) {  // diffuse.h:35-43
+__device__ BDPT_NOINLINE f3 glossy_eval_call(const BsdfRecord& b, f3 wi, f3 wo) { return glossy_eval(b, wi, wo); }
+
+// BSDF::eval. The diffuse and delta lobes are a few instructions and stay
+// inline; only the Phong-bearing lobes (powf) go through a call.
+__device__ __forceinline__ f3 bsdf_eval(const BsdfRecord& b, f3 wi, f3 wo) {
+    const int kind = b.kind;
+    if (kind == BSDF_DIFFUSE) {  // diffuse.h:35-43
         if (wi.z >= 0.f && wo.z >= 0.f) return (ld3(b.kd) * kInvPi) * wi.z;
         return mk(0.f, 0.f, 0.f);
     }
-    if (b.kind == BSDF_MIXTURE || b.kind == BSDF_PHONG) return glossy_eval(b, wi, wo);
+    if (kind == BSDF_MIXTURE || kind == BSDF_PHONG) return glossy_eval_call(b, wi, wo);
     return mk(0.f, 0.f, 0.f);  // delta lobes (perfectmirror.h:41-47, glass.h:55-59)
 }
 
@@ -423,15 +581,19 @@ __device__ __forceinline__ float phong_part_pdf(const BsdfRecord& b, f3 wi, f3 w
 
 // With specw == 0, pdfPhong * 0 = +0 (pdfPhong is finite and >= 0) and
 // 0 + pdfDiffuse * (1 - 0) == pdfDiffuse: skipping the Phong lobe is exact.
-__device__ BDPT_NOINLINE float bsdf_pdf(const BsdfRecord& b, f3 wi, f3 wo) {
-    if (b.kind == BSDF_DIFFUSE) return cosine_hemisphere_pdf(wi);  // diffuse.h:45-50
-    if (b.kind == BSDF_MIXTURE) {                                  // mixture.h:78-100
+__device__ BDPT_NOINLINE float glossy_pdf_call(const BsdfRecord& b, f3 wi, f3 wo) {
+    if (b.kind == BSDF_MIXTURE) {  // mixture.h:78-100
         const float pd = cosine_hemisphere_pdf(wi);
-        if (b.specw == 0.f) return pd;
         const float pp = phong_part_pdf(b, wi, wo);
         return (pp * b.specw) + (pd * (1.f - b.specw));
     }
-    if (b.kind == BSDF_PHONG) return phong_part_pdf(b, wi, wo);  // phong.h:73-83
+    return phong_part_pdf(b, wi, wo);  // phong.h:73-83
+}
+__device__ __forceinline__ float bsdf_pdf(const BsdfRecord& b, f3 wi, f3 wo) {
+    const int kind = b.kind;
+    if (kind == BSDF_DIFFUSE || (kind == BSDF_MIXTURE && b.specw == 0.f))  // diffuse.h:45-50
+        return cosine_hemisphere_pdf(wi);
+    if (kind == BSDF_MIXTURE || kind == BSDF_PHONG) return glossy_pdf_call(b, wi, wo);
     return 0.f;
 }
 
@@ -446,12 +608,8 @@ __device__ __forceinline__ float fresnel_dielectric(float eta_i, float eta_t, fl
 }
 
 // BSDF::sample: sets wi, returns f*cos, writes the solid-angle pdf.
-__device__ BDPT_NOINLINE f3 bsdf_sample(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
+__device__ BDPT_NOINLINE f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
     switch (b.kind) {
-        case BSDF_DIFFUSE:  // diffuse.h:52-61
-            wi = cosine_hemisphere(u);
-            pdf = cosine_hemisphere_pdf(wi);
-            return bsdf_eval(b, wi, wo);
         case BSDF_MIRROR:  // perfectmirror.h:49-59
             pdf = 1.f;
             wi = reflect_z(wo);
@@ -505,6 +663,14 @@ __device__ BDPT_NOINLINE f3 bsdf_sample(const BsdfRecord& b, f3 wo, F2 u, f3& wi
             wi = mk(0.f, 0.f, 0.f);
             return mk(0.f, 0.f, 0.f);
     }
+}
+__device__ __forceinline__ f3 bsdf_sample(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
+    if (b.kind == BSDF_DIFFUSE) {  // diffuse.h:52-61
+        wi = cosine_hemisphere(u);
+        pdf = cosine_hemisphere_pdf(wi);
+        return bsdf_eval(b, wi, wo);
+    }
+    return bsdf_sample_call(b, wo, u, wi, pdf);
 }
 
 __device__ __forceinline__ bool is_delta(const BsdfRecord& b) { return (b.type & kTypeDelta) != 0; }

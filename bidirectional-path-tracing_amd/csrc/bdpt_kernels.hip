@@ -29,7 +29,6 @@ namespace dev {
 #define BDPT_WAVES_PER_EU 3  // waves per SIMD the register allocator must leave room for
 #endif
 constexpr int kBlock = 256;
-constexpr int kStackDepth = 40;  // >= max BVH depth + 1 (checked on the host)
 constexpr int kLvFields = 16;    // p.xyz n.xyz wo.xyz tp.xyz vcm vc rr mat
 constexpr uint32_t kFlagNoEyeAccum = 0x100u;  // single-sample API: Li is returned, not added
 constexpr int kMaxStepsPerSample = 4096;      // safety bound (a legal sample needs < 900 at rrDepth 28)
@@ -41,10 +40,10 @@ struct LightStore {
     float* __restrict__ base;
     uint32_t nslots, slot;
     __device__ __forceinline__ void put(int v, int f, float x) const {
-        base[(static_cast<size_t>(v) * kLvFields + f) * nslots + slot] = x;
+        gst1(base + (static_cast<size_t>(v) * kLvFields + f) * nslots + slot, x);
     }
     __device__ __forceinline__ float get(int v, int f) const {
-        return base[(static_cast<size_t>(v) * kLvFields + f) * nslots + slot];
+        return gld1(base + (static_cast<size_t>(v) * kLvFields + f) * nslots + slot);
     }
 };
 
@@ -465,11 +464,13 @@ __device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame
 // One query for the lane's pending state, then the state advance.
 template <bool FULL, bool COUNT>
 __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
-                                     const LightStore& ls, Stack stk, Counts& cnt) {
+                                     const LightStore& ls, const Stack& stk, Counts& cnt) {
     const bool any = (L.state == ST_SPLAT || L.state == ST_NEE || L.state == ST_CONN);
     if (COUNT) cnt.c[any ? 1 : 0]++;
     float t, u, v;
+    const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     const int res = traverse<FULL, COUNT>(sc, L.ray, any, stk, t, u, v, cnt);
+    const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     bool hit = res >= 0;
     if (hit && !any) hit = (t <= L.ray.max_t && t >= L.ray.min_t);  // accel.h:133
     if (hit && !any) shade_hit(sc, res, u, v, t, L.ray.d, L.h);
@@ -508,6 +509,11 @@ __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame
     // A state-machine bug must not hang the GPU: bound the queries per sample.
     if (++L.steps > kMaxStepsPerSample && act != A_FINISH) act = A_FINISH;
     advance<COUNT>(L, act, sc, fr, fb, ls, cnt);
+    if (COUNT && first_active_lane()) {  // wave clocks in traversal / in the state advance
+        const uint64_t c2 = __builtin_amdgcn_s_memtime();
+        cnt.c[12] += static_cast<uint32_t>(c1 - c0);
+        cnt.c[13] += static_cast<uint32_t>(c2 - c1);
+    }
 }
 
 __device__ __forceinline__ void flush_counts(const Counts& cnt, unsigned long long* out) {
@@ -527,6 +533,7 @@ struct KParams {
     DevFrame fr;
     float* fb;
     float* lv;
+    uint2* gstack;  // traversal-stack overflow, (depth - kLdsStack) entries per slot
     uint32_t nslots;
     unsigned long long* work;
     unsigned long long* counters;
@@ -535,9 +542,9 @@ struct KParams {
 template <bool FULL, bool COUNT>
 __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(const KParams* __restrict__ kpp) {
     const KParams& kp = *kpp;
-    __shared__ uint32_t stack_mem[kStackDepth * kBlock];
+    __shared__ uint2 stack_mem[kLdsStack * kBlock];
     const int lane = threadIdx.x & 63;
-    const Stack stk{stack_mem + threadIdx.x, kBlock};
+    const Stack stk{stack_mem + threadIdx.x, kBlock, kp.gstack, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     const LightStore ls{kp.lv, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
@@ -546,6 +553,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     Lane L;
     L.state = ST_IDLE;
     bool exhausted = false;  // wave-uniform
+    const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
         const KParams* P = kpp;
         asm volatile("" : "+s"(P));
@@ -570,14 +578,18 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         }
         if (L.state != ST_IDLE) step<FULL, COUNT>(L, P->sc, P->fr, P->fb, ls, stk, cnt);
     }
-    if (COUNT) flush_counts(cnt, kp.counters);
+    if (COUNT) {
+        if (lane == 0) cnt.c[14] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - clock0);
+        flush_counts(cnt, kp.counters);
+    }
 }
 
 // One Integrator::render(ray, sampler) call on one lane. out = Li.xyz, draws.
 __global__ __launch_bounds__(64) void bdpt_sample_kernel(DevScene sc, DevFrame fr, float* __restrict__ fb,
-                                                         float* __restrict__ lvbuf, Ray ray, uint32_t seed,
-                                                         uint32_t draws, float* __restrict__ out) {
-    __shared__ uint32_t stack_mem[kStackDepth * 64];
+                                                         float* __restrict__ lvbuf, uint2* __restrict__ gstack,
+                                                         Ray ray, uint32_t seed, uint32_t draws,
+                                                         float* __restrict__ out) {
+    __shared__ uint2 stack_mem[kLdsStack * 64];
     if (threadIdx.x != 0) return;
     Counts cnt;
     const LightStore ls{lvbuf, 1, 0};
@@ -591,7 +603,8 @@ __global__ __launch_bounds__(64) void bdpt_sample_kernel(DevScene sc, DevFrame f
     L.state = ST_PRIMARY;
     DevFrame f1 = fr;
     f1.flags |= kFlagNoEyeAccum;  // Integrator::render returns Li; the caller accumulates it
-    while (L.state != ST_IDLE) step<false, false>(L, sc, f1, fb, ls, Stack{stack_mem, 64}, cnt);
+    const Stack stk{stack_mem, 64, gstack, 1, 0};
+    while (L.state != ST_IDLE) step<false, false>(L, sc, f1, fb, ls, stk, cnt);
     out[0] = L.Li.x, out[1] = L.Li.y, out[2] = L.Li.z;
     out[3] = __uint_as_float(L.rng.n);
 }
@@ -603,11 +616,11 @@ size_t frame_params_bytes() { return sizeof(dev::KParams); }
 
 // `dparams` is a device buffer of frame_params_bytes() owned by the caller; it
 // is filled on `stream` before the launch (stream order protects reuse).
-hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint32_t nslots,
-                        unsigned long long* work, unsigned long long* counters, int grid, hipStream_t stream,
-                        void* dparams) {
+hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                        uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
+                        hipStream_t stream, void* dparams) {
     const bool full = (fr.flags & 2u) != 0, count = (fr.flags & 1u) != 0;
-    const dev::KParams host{sc, fr, fb, lvbuf, nslots, work, counters};
+    const dev::KParams host{sc, fr, fb, lvbuf, gstack, nslots, work, counters};
     hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);
     if (e != hipSuccess) return e;
     const dev::KParams* kp = static_cast<const dev::KParams*>(dparams);
@@ -619,9 +632,10 @@ hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float*
     return hipGetLastError();
 }
 
-hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, const dev::Ray& ray,
-                         uint32_t seed, uint32_t draws, float* out, hipStream_t stream) {
-    hipLaunchKernelGGL(dev::bdpt_sample_kernel, dim3(1), dim3(64), 0, stream, sc, fr, fb, lvbuf, ray, seed, draws, out);
+hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                         const dev::Ray& ray, uint32_t seed, uint32_t draws, float* out, hipStream_t stream) {
+    hipLaunchKernelGGL(dev::bdpt_sample_kernel, dim3(1), dim3(64), 0, stream, sc, fr, fb, lvbuf, gstack, ray, seed,
+                       draws, out);
     return hipGetLastError();
 }
 
@@ -635,7 +649,7 @@ int frame_kernel_blocks_per_cu() {
     return n;
 }
 
-int frame_kernel_stack_depth() { return dev::kStackDepth; }
+int frame_kernel_lds_stack() { return dev::kLdsStack; }
 int frame_kernel_block() { return dev::kBlock; }
 int light_vertex_fields() { return dev::kLvFields; }
 

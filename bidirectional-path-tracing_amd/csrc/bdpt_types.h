@@ -1,9 +1,11 @@
 // Plain-old-data records shared by the host ingest and the HIP kernels.
 //
 // HBM layout (all arrays 16-byte aligned, read through float4 loads):
-//   tri[3*i + c]   c=0..2: (v_c.x, v_c.y, v_c.z, 0)          triangle i in BVH leaf order
-//   shade[3*i + c] c=0..2: (n_c.x, n_c.y, n_c.z, id_c)       id_0 = matID, id_1 = shapeID,
+//   tri[3*i + c]   (v0, 0), (v1 - v0, 0), (v2 - v0, 0)     triangle i in BVH leaf order; the
+//                                                            edges rounded as the reference's test forms them
+//   shade[5*i + c] c=0..2: (n_c.x, n_c.y, n_c.z, id_c)       id_0 = matID, id_1 = shapeID,
 //                                                            id_2 = primID (int bits)
+//                  c=3,4: (v1, 0), (v2, 0)                   for the hit point of a closest hit
 //   nodes[4*j + q] interior node j (2-wide, both child boxes inline):
 //       q0 = c0.min.xyz, c0.max.x   q1 = c0.max.yz, c1.min.xy
 //       q2 = c1.min.z, c1.max.xyz   q3 = (link0, link1, 0, 0) as uint bits

@@ -169,6 +169,43 @@ __device__ BDPT_NOINLINE float glibc_sincosf(float y, int which) {
     }
     return sincos_poly(x * s, x * x, sincos_poly_table(neg), which ? (n ^ 1) : n);
 }
+// sinf(y) and cosf(y) from one range reduction: each output is bit-identical
+// to the corresponding single call above (same reduction, same polynomial).
+struct SinCos {
+    float s, c;
+};
+__device__ BDPT_NOINLINE SinCos glibc_sincosf2(float y) {
+    double x = y;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+        double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return SinCos{y, 1.0f};
+        const SinCosPoly p = sincos_poly_table(false);
+        return SinCos{sincos_poly(x, x2, p, 0), sincos_poly(x, x2, p, 1)};
+    }
+    int n;
+    double s;
+    bool neg;
+    if (abstop12(y) < abstop12(120.0f)) {
+        double r = x * 0x1.45f306dc9c883p+23;
+        n = (static_cast<int32_t>(r) + 0x800000) >> 24;
+        x = __builtin_fma(-static_cast<double>(n), 0x1.921fb54442d18p+0, x);
+        s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
+        neg = (n & 2) != 0;
+    } else if (abstop12(y) < abstop12(__builtin_inff())) {
+        uint32_t xi = f2u(y);
+        int sign = xi >> 31;
+        x = sincos_reduce_large(xi, &n);
+        int q = n + sign;
+        s = ((q & 3) == 1 || (q & 3) == 2) ? -1.0 : 1.0;
+        neg = (q & 2) != 0;
+    } else {
+        const float nan = (y - y) / (y - y);
+        return SinCos{nan, nan};
+    }
+    const SinCosPoly p = sincos_poly_table(neg);
+    return SinCos{sincos_poly(x * s, x * x, p, n), sincos_poly(x * s, x * x, p, n ^ 1)};
+}
+
 __device__ __forceinline__ float glibc_sinf(float x) { return glibc_sincosf(x, 0); }
 __device__ __forceinline__ float glibc_cosf(float x) { return glibc_sincosf(x, 1); }
 

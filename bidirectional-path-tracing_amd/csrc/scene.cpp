@@ -1,6 +1,7 @@
 // Host-side scene ingest (see scene.hpp). Compiled with -ffp-contract=off:
 // every float expression below must round exactly like the reference's.
 #include "scene.hpp"
+#include "wide_bvh.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -609,16 +610,22 @@ bool build_device_layout(const HostScene& s, DeviceLayout& out, std::string& err
     };
     out = DeviceLayout();
     out.tri.resize(3 * n);
-    out.shade.resize(3 * n);
+    out.shade.resize(5 * n);
     for (size_t i = 0; i < n; i++) {
         const size_t t = static_cast<size_t>(s.order[i]);
         const int32_t ids[3] = {s.tri_mat[t], s.tri_shape[t], s.tri_prim[t]};
+        const float* v = &s.pos[9 * t];
+        // v0 and the edges e1 = v1 - v0, e2 = v2 - v0 exactly as rayTriangleIntersect
+        // forms them in float (core.h:381-382), so the device test skips 6 subtractions.
+        out.tri[3 * i + 0] = {v[0], v[1], v[2], 0.f};
+        out.tri[3 * i + 1] = {v[3] - v[0], v[4] - v[1], v[5] - v[2], 0.f};
+        out.tri[3 * i + 2] = {v[6] - v[0], v[7] - v[1], v[8] - v[2], 0.f};
         for (int c = 0; c < 3; c++) {
-            const float* p = &s.pos[9 * t + 3 * c];
             const float* q = &s.nrm[9 * t + 3 * c];
-            out.tri[3 * i + c] = {p[0], p[1], p[2], 0.f};
-            out.shade[3 * i + c] = {q[0], q[1], q[2], bits(ids[c])};
+            out.shade[5 * i + c] = {q[0], q[1], q[2], bits(ids[c])};
         }
+        out.shade[5 * i + 3] = {v[3], v[4], v[5], 0.f};
+        out.shade[5 * i + 4] = {v[6], v[7], v[8], 0.f};
     }
     // Flat preorder tree -> interior records holding both child boxes.
     std::vector<int32_t> rec(s.nodes.size(), -1);
@@ -642,6 +649,12 @@ bool build_device_layout(const HostScene& s, DeviceLayout& out, std::string& err
         r[3] = {bits(static_cast<int32_t>(link_of(i + 1))), bits(static_cast<int32_t>(link_of(i + s.nodes[i].right_offset))),
                 0.f, 0.f};
     }
+    WideBvh wb;
+    if (!build_wide_bvh(s.nodes, wb, err)) return false;
+    out.wnodes.swap(wb.nodes);
+    out.wroot_link = wb.root_link;
+    out.wmax_stack = wb.max_stack;
+    out.wdepth = wb.depth;
     out.bsdfs = s.bsdfs;
     for (const Emitter& e : s.emitters) {
         EmitterRecord r{};

@@ -63,9 +63,12 @@ bool load_obj_scene(const std::string& obj_path, HostScene& out, std::string& er
 // Flattened arrays uploaded to HBM (layouts documented in bdpt_types.h).
 struct DeviceLayout {
     std::vector<float4_t> tri;      // 3 per triangle, BVH leaf order
-    std::vector<float4_t> shade;    // 3 per triangle, BVH leaf order
-    std::vector<float4_t> nodes;    // 4 per interior node
+    std::vector<float4_t> shade;    // 5 per triangle, BVH leaf order
+    std::vector<float4_t> nodes;    // 4 per interior node (the reference's binary tree)
     uint32_t root_link = 0;
+    std::vector<float4_t> wnodes;   // 8 per 4-wide node over the same leaves (wide_bvh.hpp)
+    uint32_t wroot_link = 0;
+    int wmax_stack = 0, wdepth = 0;
     std::vector<BsdfRecord> bsdfs;
     std::vector<EmitterRecord> emitters;
     std::vector<float4_t> emit_tri; // 5 per emitter face, shape face order

@@ -1,0 +1,230 @@
+// Binned-SAH 4-wide hierarchy over the reference's BVH leaves (see wide_bvh.hpp).
+#include "wide_bvh.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+
+#include "scene.hpp"
+
+namespace bdpt {
+namespace {
+
+struct Box {
+    float lo[3], hi[3];
+    void clear() {
+        for (int a = 0; a < 3; a++) lo[a] = __builtin_inff(), hi[a] = -__builtin_inff();
+    }
+    void grow(const Box& b) {
+        for (int a = 0; a < 3; a++) lo[a] = std::min(lo[a], b.lo[a]), hi[a] = std::max(hi[a], b.hi[a]);
+    }
+    double area() const {
+        const double x = std::max(0.0, double(hi[0]) - lo[0]), y = std::max(0.0, double(hi[1]) - lo[1]),
+                     z = std::max(0.0, double(hi[2]) - lo[2]);
+        return 2.0 * (x * y + y * z + z * x);
+    }
+};
+
+struct Leaf {
+    Box box;
+    float c[3];
+    uint32_t link;
+};
+
+struct BNode {  // binary build node
+    Box box;
+    int left = -1, right = -1;  // children (binary node ids), -1 for a leaf
+    int leaf = -1;              // index into leaves when a leaf
+};
+
+constexpr int kBins = 32;
+constexpr int kMaxBinaryDepth = 96;
+
+class Builder {
+   public:
+    explicit Builder(std::vector<Leaf>& leaves) : L(leaves) {}
+    std::vector<BNode> nodes;
+    int max_depth = 0;
+    bool median_only = false;
+
+    int build(int b, int e, int depth) {
+        max_depth = std::max(max_depth, depth);
+        const int id = static_cast<int>(nodes.size());
+        nodes.emplace_back();
+        Box box;
+        box.clear();
+        for (int i = b; i < e; i++) box.grow(L[i].box);
+        nodes[id].box = box;
+        if (e - b == 1) {
+            nodes[id].leaf = b;
+            return id;
+        }
+        const int mid = split(b, e);
+        const int l = build(b, mid, depth + 1);
+        const int r = build(mid, e, depth + 1);
+        nodes[id].left = l;
+        nodes[id].right = r;
+        return id;
+    }
+
+   private:
+    std::vector<Leaf>& L;
+
+    int median(int b, int e, int axis) {
+        const int mid = (b + e) / 2;
+        std::nth_element(L.begin() + b, L.begin() + mid, L.begin() + e,
+                         [axis](const Leaf& x, const Leaf& y) { return x.c[axis] < y.c[axis]; });
+        return mid;
+    }
+
+    int split(int b, int e) {
+        float cl[3], ch[3];
+        for (int a = 0; a < 3; a++) cl[a] = __builtin_inff(), ch[a] = -__builtin_inff();
+        for (int i = b; i < e; i++)
+            for (int a = 0; a < 3; a++) cl[a] = std::min(cl[a], L[i].c[a]), ch[a] = std::max(ch[a], L[i].c[a]);
+        int wide_axis = 0;
+        for (int a = 1; a < 3; a++)
+            if (ch[a] - cl[a] > ch[wide_axis] - cl[wide_axis]) wide_axis = a;
+        if (median_only || !(ch[wide_axis] > cl[wide_axis])) return median(b, e, wide_axis);
+        double best = __builtin_inf();
+        int best_axis = -1, best_bin = -1;
+        for (int a = 0; a < 3; a++) {
+            if (!(ch[a] > cl[a])) continue;
+            const double scale = kBins / (double(ch[a]) - cl[a]);
+            Box bb[kBins];
+            int cnt[kBins] = {};
+            for (int k = 0; k < kBins; k++) bb[k].clear();
+            for (int i = b; i < e; i++) {
+                int k = static_cast<int>((double(L[i].c[a]) - cl[a]) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                cnt[k]++;
+                bb[k].grow(L[i].box);
+            }
+            double right_area[kBins];
+            int right_cnt[kBins];
+            Box acc;
+            acc.clear();
+            int n = 0;
+            for (int k = kBins - 1; k > 0; k--) {
+                acc.grow(bb[k]);
+                n += cnt[k];
+                right_area[k] = acc.area();
+                right_cnt[k] = n;
+            }
+            acc.clear();
+            n = 0;
+            for (int k = 0; k < kBins - 1; k++) {
+                acc.grow(bb[k]);
+                n += cnt[k];
+                if (n == 0 || right_cnt[k + 1] == 0) continue;
+                const double cost = acc.area() * n + right_area[k + 1] * right_cnt[k + 1];
+                if (cost < best) best = cost, best_axis = a, best_bin = k;
+            }
+        }
+        if (best_axis < 0) return median(b, e, wide_axis);
+        const double scale = kBins / (double(ch[best_axis]) - cl[best_axis]);
+        const float lo = cl[best_axis];
+        auto it = std::partition(L.begin() + b, L.begin() + e, [&](const Leaf& x) {
+            int k = static_cast<int>((double(x.c[best_axis]) - lo) * scale);
+            k = std::min(std::max(k, 0), kBins - 1);
+            return k <= best_bin;
+        });
+        const int mid = static_cast<int>(it - L.begin());
+        if (mid == b || mid == e) return median(b, e, wide_axis);
+        return mid;
+    }
+};
+
+float u2f(uint32_t u) {
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+}  // namespace
+
+bool build_wide_bvh(const std::vector<FlatNode>& flat, WideBvh& out, std::string& err) {
+    out = WideBvh();
+    if (flat.empty()) {
+        err = "empty BVH";
+        return false;
+    }
+    std::vector<Leaf> leaves;
+    for (const FlatNode& n : flat) {
+        if (n.right_offset != 0) continue;
+        Leaf l;
+        for (int a = 0; a < 3; a++) {
+            l.box.lo[a] = n.bmin[a];
+            l.box.hi[a] = n.bmax[a];
+            l.c[a] = 0.5f * (n.bmin[a] + n.bmax[a]);
+        }
+        l.link = make_leaf_link(n.start, n.nprims);
+        leaves.push_back(l);
+    }
+    out.leaves = static_cast<int64_t>(leaves.size());
+    if (flat[0].right_offset == 0) {  // the whole scene is one leaf: the reference tests no box
+        out.root_link = leaves[0].link;
+        return true;
+    }
+    Builder B(leaves);
+    B.build(0, static_cast<int>(leaves.size()), 0);
+    if (B.max_depth > kMaxBinaryDepth) {  // degenerate SAH splits: fall back to a balanced tree
+        Builder M(leaves);
+        M.median_only = true;
+        M.build(0, static_cast<int>(leaves.size()), 0);
+        B.nodes.swap(M.nodes);
+        B.max_depth = M.max_depth;
+    }
+    const std::vector<BNode>& bn = B.nodes;
+
+    // Collapse to 4-wide: repeatedly open the interior child of largest area.
+    int max_stack = 0, max_depth = 0;
+    std::function<uint32_t(int, int, int)> emit = [&](int id, int depth, int stack_above) -> uint32_t {
+        std::vector<int> ch = {bn[id].left, bn[id].right};
+        while (static_cast<int>(ch.size()) < kWideArity) {
+            int pick = -1;
+            double area = -1.0;
+            for (int k = 0; k < static_cast<int>(ch.size()); k++)
+                if (bn[ch[k]].leaf < 0 && bn[ch[k]].box.area() > area) area = bn[ch[k]].box.area(), pick = k;
+            if (pick < 0) break;
+            const int c = ch[pick];
+            ch[pick] = bn[c].left;
+            ch.push_back(bn[c].right);
+        }
+        const uint32_t me = static_cast<uint32_t>(out.nodes.size() / 8);
+        out.nodes.resize(out.nodes.size() + 8);
+        max_depth = std::max(max_depth, depth + 1);
+        const int stack_here = stack_above + static_cast<int>(ch.size()) - 1;
+        max_stack = std::max(max_stack, stack_here);
+        uint32_t links[kWideArity];
+        Box boxes[kWideArity];
+        for (int k = 0; k < kWideArity; k++) {
+            if (k >= static_cast<int>(ch.size())) {
+                links[k] = kEmptyLink;
+                for (int a = 0; a < 3; a++) boxes[k].lo[a] = boxes[k].hi[a] = 0.f;
+                continue;
+            }
+            const BNode& c = bn[ch[k]];
+            boxes[k] = c.box;
+            links[k] = c.leaf >= 0 ? leaves[c.leaf].link : emit(ch[k], depth + 1, stack_here);
+        }
+        float4_t* r = &out.nodes[8 * static_cast<size_t>(me)];
+        for (int a = 0; a < 3; a++) {
+            r[2 * a] = {boxes[0].lo[a], boxes[1].lo[a], boxes[2].lo[a], boxes[3].lo[a]};
+            r[2 * a + 1] = {boxes[0].hi[a], boxes[1].hi[a], boxes[2].hi[a], boxes[3].hi[a]};
+        }
+        r[6] = {u2f(links[0]), u2f(links[1]), u2f(links[2]), u2f(links[3])};
+        r[7] = {0.f, 0.f, 0.f, 0.f};
+        return me;
+    };
+    out.root_link = emit(0, 0, 0);
+    out.max_stack = max_stack;
+    out.depth = max_depth;
+    if (out.root_link != 0) {
+        err = "wide BVH root must be node 0";
+        return false;
+    }
+    return true;
+}
+
+}  // namespace bdpt

@@ -61,6 +61,9 @@ typedef struct bdpt_ctx bdpt_ctx;     /* device context (one HIP device) */
 typedef struct {
     int64_t triangles, bvh_nodes, shapes, materials, emitters, bvh_max_depth;
     int64_t device_bytes; /* HBM bytes of the uploaded scene arrays */
+    int64_t bvh_leaves;   /* reference BVH leaves (<= 4 triangles each) */
+    int64_t wide_nodes;   /* 4-wide traversal nodes built over those leaves */
+    int64_t wide_depth, wide_max_stack;
 } bdpt_scene_info;
 
 typedef struct {
@@ -80,12 +83,14 @@ typedef struct {
     uint32_t flags;        /* BDPT_FLAG_* */
 } bdpt_frame_params;
 
-#define BDPT_NUM_COUNTERS 12
+#define BDPT_NUM_COUNTERS 16
 /* counters: [0] closest-hit rays, [1] shadow rays, [2] interior-node visits,
  * [3] triangle tests, [4] light vertices stored, [5] light-vertex reads,
  * [6] camera splats, [7] RNG draws; SIMD-efficiency probes: [8] traversal
  * iterations summed over lanes, [9] the same counted once per wave, [10]
- * state-machine actions summed over lanes, [11] action executions per wave. */
+ * state-machine actions summed over lanes, [11] action executions per wave;
+ * wave clocks (s_memtime, summed over waves): [12] in traversal, [13] in the
+ * state advance, [14] whole persistent loop; [15] exact slab fallbacks. */
 typedef struct {
     double kernel_ms;      /* HIP-event time of the render kernel(s) of the last call */
     int64_t samples;       /* camera samples rendered by the last call */

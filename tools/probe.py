@@ -23,6 +23,9 @@ c, n = st["counters"], st["samples"]
 out = {k: round(v / n, 3) for k, v in c.items()}
 out["trav_simd_eff"] = round(c["trav_lane_iters"] / max(64 * c["trav_wave_iters"], 1), 4)
 out["shade_simd_eff"] = round(c["shade_lane_actions"] / max(64 * c["shade_wave_actions"], 1), 4)
+lc = max(c["loop_clocks"], 1)
+out["trav_clock_frac"] = round(c["trav_clocks"] / lc, 4)
+out["shade_clock_frac"] = round(c["shade_clocks"] / lc, 4)
 out["kernel_ms"] = round(t_plain, 3)
 out["msamples_per_s"] = round(n / t_plain * 1e-3, 3)
 print(json.dumps({"scene": name, "W": W, "H": H, "spp": spp, **out}))
