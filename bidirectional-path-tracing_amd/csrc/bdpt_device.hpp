@@ -30,6 +30,9 @@ __device__ __forceinline__ float4 gld4(const float4* p) {
 }
 __device__ __forceinline__ float gld1(const float* p) { return *(const __attribute__((address_space(1))) float*)(p); }
 __device__ __forceinline__ void gst1(float* p, float x) { *(__attribute__((address_space(1))) float*)(p) = x; }
+__device__ __forceinline__ void gst4(float4* p, float4 x) {
+    *(__attribute__((address_space(1))) v4f_t*)(p) = v4f_t{x.x, x.y, x.z, x.w};
+}
 
 struct DevScene {
     const float4* __restrict__ tri;
@@ -62,7 +65,7 @@ struct Ray {
 
 // Hit record = the parts of SurfaceInteraction (core.h:173-180) the path reads.
 struct Hit {
-    f3 p, wo, wi;
+    f3 p, wo;
     f3 s, t, n;  // frameNs
     float dist;
     int mat, shape;
@@ -312,16 +315,35 @@ constexpr uint32_t kEmptyLinkDev = 0xffffffffu;  // unused 4-wide child slot
 struct Stack {
     uint2* lds;
     int stride;
-    uint2* gbl;  // entry k >= kLdsStack at gbl[(k - kLdsStack) * nslots + slot]
+    int nlds;    // entries held in LDS
+    uint2* gbl;  // entry k >= nlds at gbl[(k - nlds) * nslots + slot]
     uint32_t nslots, slot;
     __device__ __forceinline__ void put(int k, uint32_t link, float tn) const {
         const uint2 e = make_uint2(link, __float_as_uint(tn));
-        if (k < kLdsStack) lds[k * stride] = e;
-        else gbl[static_cast<size_t>(k - kLdsStack) * nslots + slot] = e;
+        if (k < nlds) lds[k * stride] = e;
+        else gbl[static_cast<size_t>(k - nlds) * nslots + slot] = e;
     }
     __device__ __forceinline__ uint2 get(int k) const {
-        if (k < kLdsStack) return lds[k * stride];
-        return gbl[static_cast<size_t>(k - kLdsStack) * nslots + slot];
+        if (k < nlds) return lds[k * stride];
+        return gbl[static_cast<size_t>(k - nlds) * nslots + slot];
+    }
+};
+
+// Link-only stack for the binary reference traversal in kernels that keep a
+// deeper LDS column of 4-byte entries (entry k of thread x at lds[k * stride]).
+struct LinkStack {
+    uint32_t* lds;
+    int stride;
+    int nlds;
+    uint32_t* gbl;  // entry k >= nlds at gbl[(k - nlds) * nslots + slot]
+    uint32_t nslots, slot;
+    __device__ __forceinline__ void put(int k, uint32_t link, float) const {
+        if (k < nlds) lds[k * stride] = link;
+        else gbl[static_cast<size_t>(k - nlds) * nslots + slot] = link;
+    }
+    __device__ __forceinline__ uint2 get(int k) const {
+        if (k < nlds) return make_uint2(lds[k * stride], 0u);
+        return make_uint2(gbl[static_cast<size_t>(k - nlds) * nslots + slot], 0u);
     }
 };
 
@@ -379,8 +401,8 @@ struct TravResult {
 // the slab test is not monotone) and for BDPT_FLAG_FULL_TRAVERSAL (cull =
 // false: every box the reference visits). Out of line, arguments by value
 // (nothing of the caller's lives in scratch).
-template <bool COUNT>
-__device__ BDPT_NOINLINE TravResult traverse_binary(const DevScene& sc, Ray r, bool any, bool cull, Stack stk) {
+template <bool COUNT, typename StackT>
+__device__ BDPT_NOINLINE TravResult traverse_binary(const DevScene& sc, Ray r, bool any, bool cull, StackT stk) {
     TravResult res{-1, r.max_t, 0.f, 0.f, 0u, 0u, 0u};
     uint32_t link = sc.root_link;
     int sp = 0;
@@ -422,95 +444,110 @@ __device__ __forceinline__ int child_fast(float lx, float hx, float ly, float hy
     return slab_fast(lx, ly, lz, hx, hy, hz, o, inv, tn, tf);
 }
 
-// Closest-hit / occlusion query over the 4-wide hierarchy (wide_bvh.hpp).
+// Closest-hit / occlusion query over the 4-wide hierarchy (wide_bvh.hpp),
+// written as a resumable step so persistent kernels can refill finished lanes.
 // Interior children: a conservative test (ambiguous counts as a hit) — any box
 // containing a reachable leaf box passes the reference's test, so it is never
 // rejected. Leaf children (the reference's leaves): decided exactly (fast
 // test, then the cross pairs, then the reference's own divisions). Children
 // are visited near-first; stacked entries carry their entry distance and are
 // dropped on pop once a closer hit exists.
+struct TravState {
+    uint32_t link;
+    int sp;
+    int best;
+    float best_t, best_u, best_v;
+};
+
+__device__ __forceinline__ TravState trav_begin(const DevScene& sc, const Ray& r) {
+    return TravState{sc.wroot_link, 0, -1, r.max_t, 0.f, 0.f};
+}
+
+// One loop iteration (a 4-wide node or a leaf, then the pop). Returns true
+// when the query is complete (result in ts.best / best_t / best_u / best_v).
+template <bool COUNT>
+__device__ __forceinline__ bool trav_step(const DevScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
+                                          const Stack& stk, Counts& cnt) {
+    if (COUNT) {
+        cnt.c[8]++;
+        if (first_active_lane()) cnt.c[9]++;
+    }
+    const uint32_t link = ts.link;
+    if (link & kLeafBit) {
+        if (leaf_tests<COUNT>(sc, link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return true;
+    } else {
+        if (COUNT) cnt.c[2]++;
+        const float4* nd = sc.wnodes + 8 * static_cast<size_t>(link);
+        const float4 lx = gld4(nd), hx = gld4(nd + 1), ly = gld4(nd + 2), hy = gld4(nd + 3), lz = gld4(nd + 4),
+                     hz = gld4(nd + 5), lk = gld4(nd + 6);
+        const float far = cull_far(any ? r.max_t : ts.best_t);
+        float key[4];
+        uint32_t lnk[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float clx = (&lx.x)[c], chx = (&hx.x)[c], cly = (&ly.x)[c], chy = (&hy.x)[c], clz = (&lz.x)[c],
+                        chz = (&hz.x)[c];
+            const uint32_t l = __float_as_uint((&lk.x)[c]);
+            float tn, tf;
+            int d = slab_fast(clx, cly, clz, chx, chy, chz, r.o, ri.inv, tn, tf);
+            const bool leaf = (l & kLeafBit) != 0 && l != kEmptyLinkDev;
+            if (d == kSlabAmbiguous && leaf) {
+                d = slab_cross(clx, cly, clz, chx, chy, chz, r.o, ri.inv);
+                if (d == kSlabAmbiguous) {
+                    if (COUNT) cnt.c[15]++;
+                    float en, ex;
+                    d = slab(clx, cly, clz, chx, chy, chz, r, en, ex) ? kSlabHit : kSlabMiss;
+                }
+            }
+            const bool hit = l != kEmptyLinkDev && d != kSlabMiss && !(tn > far) && !(tf < kCullNear);
+            key[c] = hit ? tn : __builtin_inff();
+            lnk[c] = hit ? l : kEmptyLinkDev;
+        }
+        // near-first order: sorting network on (key, link)
+#define BDPT_CE(a, b)                                                       \
+    {                                                                       \
+        const bool sw = key[b] < key[a];                                    \
+        const float k0 = sw ? key[b] : key[a], k1 = sw ? key[a] : key[b];   \
+        const uint32_t l0 = sw ? lnk[b] : lnk[a], l1 = sw ? lnk[a] : lnk[b]; \
+        key[a] = k0, key[b] = k1, lnk[a] = l0, lnk[b] = l1;                 \
+    }
+        BDPT_CE(0, 1) BDPT_CE(2, 3) BDPT_CE(0, 2) BDPT_CE(1, 3) BDPT_CE(1, 2)
+#undef BDPT_CE
+        if (lnk[0] != kEmptyLinkDev) {
+            if (lnk[3] != kEmptyLinkDev) stk.put(ts.sp++, lnk[3], key[3]);
+            if (lnk[2] != kEmptyLinkDev) stk.put(ts.sp++, lnk[2], key[2]);
+            if (lnk[1] != kEmptyLinkDev) stk.put(ts.sp++, lnk[1], key[1]);
+            ts.link = lnk[0];
+            return false;
+        }
+    }
+    // pop the nearest pending entry that can still hold a closer hit
+    while (ts.sp > 0) {
+        const uint2 e = stk.get(--ts.sp);
+        if (!(__uint_as_float(e.y) > cull_far(any ? r.max_t : ts.best_t))) {
+            ts.link = e.x;
+            return false;
+        }
+    }
+    return true;
+}
+
 template <bool FULL, bool COUNT>
 __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool any, const Stack& stk, float& bt,
                                         float& bu, float& bv, Counts& cnt) {
     if (r.min_t > r.max_t) return -1;  // the root's entry mint is min_t (bvh.h:277, :287)
     const RayInv ri = ray_inv(r);
     if (FULL || !ri.fast) {
-        const TravResult q = traverse_binary<COUNT>(sc, r, any, !FULL, stk);
+        const TravResult q = traverse_binary<COUNT, Stack>(sc, r, any, !FULL, stk);
         if (COUNT) cnt.c[2] += q.nodes, cnt.c[3] += q.tris, cnt.c[15] += q.exact;
         bt = q.t, bu = q.u, bv = q.v;
         return q.best;
     }
-    float best_t = r.max_t, best_u = 0.f, best_v = 0.f;
-    int best = -1;
-    uint32_t link = sc.wroot_link;
-    int sp = 0;
-    for (;;) {
-        if (COUNT) {
-            cnt.c[8]++;
-            if (first_active_lane()) cnt.c[9]++;
-        }
-        if (link & kLeafBit) {
-            if (leaf_tests<COUNT>(sc, link, r, any, best_t, best, best_u, best_v, cnt.c[3])) break;
-        } else {
-            if (COUNT) cnt.c[2]++;
-            const float4* nd = sc.wnodes + 8 * static_cast<size_t>(link);
-            const float4 lx = gld4(nd), hx = gld4(nd + 1), ly = gld4(nd + 2), hy = gld4(nd + 3), lz = gld4(nd + 4),
-                         hz = gld4(nd + 5), lk = gld4(nd + 6);
-            const float far = cull_far(any ? r.max_t : best_t);
-            float key[4];
-            uint32_t lnk[4];
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const float clx = (&lx.x)[c], chx = (&hx.x)[c], cly = (&ly.x)[c], chy = (&hy.x)[c],
-                            clz = (&lz.x)[c], chz = (&hz.x)[c];
-                const uint32_t l = __float_as_uint((&lk.x)[c]);
-                float tn, tf;
-                int d = child_fast(clx, chx, cly, chy, clz, chz, r.o, ri.inv, tn, tf);
-                const bool leaf = (l & kLeafBit) != 0 && l != kEmptyLinkDev;
-                if (d == kSlabAmbiguous && leaf) {
-                    d = slab_cross(clx, cly, clz, chx, chy, chz, r.o, ri.inv);
-                    if (d == kSlabAmbiguous) {
-                        if (COUNT) cnt.c[15]++;
-                        float en, ex;
-                        d = slab(clx, cly, clz, chx, chy, chz, r, en, ex) ? kSlabHit : kSlabMiss;
-                    }
-                }
-                const bool hit = l != kEmptyLinkDev && d != kSlabMiss && !(tn > far) && !(tf < kCullNear);
-                key[c] = hit ? tn : __builtin_inff();
-                lnk[c] = hit ? l : kEmptyLinkDev;
-            }
-            // near-first order: sorting network on (key, link)
-#define BDPT_CE(a, b)                                                   \
-    {                                                                   \
-        const bool sw = key[b] < key[a];                                \
-        const float k0 = sw ? key[b] : key[a], k1 = sw ? key[a] : key[b]; \
-        const uint32_t l0 = sw ? lnk[b] : lnk[a], l1 = sw ? lnk[a] : lnk[b]; \
-        key[a] = k0, key[b] = k1, lnk[a] = l0, lnk[b] = l1;             \
+    TravState ts = trav_begin(sc, r);
+    while (!trav_step<COUNT>(sc, r, ri, any, ts, stk, cnt)) {
     }
-            BDPT_CE(0, 1) BDPT_CE(2, 3) BDPT_CE(0, 2) BDPT_CE(1, 3) BDPT_CE(1, 2)
-#undef BDPT_CE
-            if (lnk[0] != kEmptyLinkDev) {
-                if (lnk[3] != kEmptyLinkDev) stk.put(sp++, lnk[3], key[3]);
-                if (lnk[2] != kEmptyLinkDev) stk.put(sp++, lnk[2], key[2]);
-                if (lnk[1] != kEmptyLinkDev) stk.put(sp++, lnk[1], key[1]);
-                link = lnk[0];
-                continue;
-            }
-        }
-        // pop the nearest pending entry that can still hold a closer hit
-        bool found = false;
-        while (sp > 0) {
-            const uint2 e = stk.get(--sp);
-            if (!(__uint_as_float(e.y) > cull_far(any ? r.max_t : best_t))) {
-                link = e.x;
-                found = true;
-                break;
-            }
-        }
-        if (!found) break;
-    }
-    bt = best_t, bu = best_u, bv = best_v;
-    return best;
+    bt = ts.best_t, bu = ts.best_u, bv = ts.best_v;
+    return ts.best;
 }
 
 // AcceleratorBVH::intersect's shading of a closest hit (accel.h:133-166).
@@ -523,7 +560,6 @@ __device__ __forceinline__ void shade_hit(const DevScene& sc, int i, float u, fl
     h.n = normalize((xyz(s0) * w + xyz(s1) * u) + xyz(s2) * v);
     make_frame(h.n, h.s, h.t);
     h.wo = to_local(h.s, h.t, h.n, -dir);
-    h.wi = mk(0.f, 0.f, 0.f);
     h.dist = t;
     h.mat = __float_as_int(s0.w);
     h.shape = __float_as_int(s1.w);

@@ -1,0 +1,509 @@
+// The BDPT path state machine shared by the HIP kernels: one camera sample
+// (pixel, k) of BDPTIntegrator::render (reference src/integrators/bdpt.h:219-241)
+// as a sequence of ray queries. A Lane holds the sample's state between
+// queries; resolve() applies a query's result and advance() runs the
+// integrator until the lane needs its next query (or finishes the sample).
+// The megakernel (bdpt_kernels.hip) keeps Lanes in registers; the wavefront
+// kernels (bdpt_wavefront.hip) keep them in HBM between passes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "bdpt_device.hpp"
+
+namespace bdpt {
+namespace dev {
+
+
+constexpr int kLvFields = 16;    // p vcm n vc wo rr tp mat
+constexpr uint32_t kFlagNoEyeAccum = 0x100u;  // single-sample API: Li is returned, not added
+constexpr int kMaxStepsPerSample = 4096;      // safety bound (a legal sample needs < 900 at rrDepth 28)
+
+// Light-vertex scratch, one contiguous record per lane: vertex v of slot s is
+// the four float4 at lv[(s * maxv + v) * 4 + q] — (p, vcm) (n, vc) (wo, rr)
+// (tp, mat). A lane reads or writes a whole 64-byte vertex from one cache
+// line; the divergent shading code touches no line it does not use.
+struct LightStore {
+    float4* __restrict__ base;
+    uint32_t maxv, slot;
+    __device__ __forceinline__ float4* at(int v) const {
+        return base + (static_cast<size_t>(slot) * maxv + static_cast<uint32_t>(v)) * 4;
+    }
+};
+__device__ __forceinline__ LightStore light_store(float* lv, int rr_depth, uint32_t slot) {
+    return LightStore{reinterpret_cast<float4*>(lv), static_cast<uint32_t>(rr_depth > 1 ? rr_depth - 1 : 1), slot};
+}
+
+struct Vertex {  // PathVertex (bdpt.h:24-35)
+    f3 p, s, t, n, wo, tp;
+    float vcm, vc, rr;
+    int mat;
+};
+
+__device__ __forceinline__ void store_vertex(const LightStore& ls, int v, const Hit& h, f3 tp, float vcm, float vc,
+                                             float rr) {
+    float4* q = ls.at(v);
+    gst4(q, make_float4(h.p.x, h.p.y, h.p.z, vcm));
+    gst4(q + 1, make_float4(h.n.x, h.n.y, h.n.z, vc));
+    gst4(q + 2, make_float4(h.wo.x, h.wo.y, h.wo.z, rr));
+    gst4(q + 3, make_float4(tp.x, tp.y, tp.z, __int_as_float(h.mat)));
+}
+
+__device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
+    const float4* q = ls.at(v);
+    const float4 a = gld4(q), b = gld4(q + 1), c = gld4(q + 2), d = gld4(q + 3);
+    Vertex x;
+    x.p = xyz(a), x.vcm = a.w;
+    x.n = xyz(b), x.vc = b.w;
+    x.wo = xyz(c), x.rr = c.w;
+    x.tp = xyz(d), x.mat = __float_as_int(d.w);
+    make_frame(x.n, x.s, x.t);  // Frame(n) is a pure function of n: identical s, t
+    return x;
+}
+
+// ContinuePathRandomWalk (bdpt.h:243-291): BSDF sample (2 draws), throughput,
+// vc / vcm recursion (Georgiev VCM Eqs. 52-54) and the next ray.
+__device__ __forceinline__ bool continue_walk(const BsdfRecord& b, const Hit& h, LazyMT& rng, f3& tp, int& depth,
+                                              float& vc, float& vcm, Ray& ray) {
+    const float rrp = 1.f;  // NO_RR (bdpt.h:18)
+    const bool delta = is_delta(b);
+    float pdf;
+    f3 wi;
+    const f3 f = bsdf_sample(b, h.wo, next2(rng), wi, pdf);
+    pdf *= rrp;
+    const float absCosOut = fabsf(wi.z);
+    if (is_zero(f)) return false;
+    tp = tp * (f * (1.f / pdf));
+    depth++;
+    const float prevRev = delta ? pdf : bsdf_pdf(b, h.wo, wi) * rrp;  // pdf of the swapped (wo, wi)
+    if (delta) {
+        vc = (absCosOut / pdf) * (prevRev * vc);
+        vcm = 0.f;
+    } else {
+        vc = (absCosOut / pdf) * (vcm + prevRev * vc);
+        vcm = 1.f / pdf;
+    }
+    ray = Ray{h.p, to_world(h.s, h.t, h.n, wi), kEpsilon, 3.402823466e+38f};  // FLT_MAX (core.h:120)
+    return true;
+}
+
+// splatToImagePlane (bdpt.h:485-496): worldToCamera, cameraToClip, /w, NDCToScreen.
+__device__ __forceinline__ void splat_pixel(const CameraConstants& c, f3 p, int& x, int& y) {
+    const float* m = c.w2c;
+    float a0 = (m[0] * p.x + m[4] * p.y) + (m[8] * p.z + m[12] * 1.f);
+    float a1 = (m[1] * p.x + m[5] * p.y) + (m[9] * p.z + m[13] * 1.f);
+    float a2 = (m[2] * p.x + m[6] * p.y) + (m[10] * p.z + m[14] * 1.f);
+    float a3 = (m[3] * p.x + m[7] * p.y) + (m[11] * p.z + m[15] * 1.f);
+    m = c.c2clip;
+    float b0 = (m[0] * a0 + m[4] * a1) + (m[8] * a2 + m[12] * a3);
+    float b1 = (m[1] * a0 + m[5] * a1) + (m[9] * a2 + m[13] * a3);
+    float b2 = (m[2] * a0 + m[6] * a1) + (m[10] * a2 + m[14] * a3);
+    float b3 = (m[3] * a0 + m[7] * a1) + (m[11] * a2 + m[15] * a3);
+    const float w = b3;
+    b0 = b0 / w, b1 = b1 / w, b2 = b2 / w, b3 = b3 / w;
+    m = c.ndc2screen;
+    const float d0 = (m[0] * b0 + m[4] * b1) + (m[8] * b2 + m[12] * b3);
+    const float d1 = (m[1] * b0 + m[5] * b1) + (m[9] * b2 + m[13] * b3);
+    x = x86_trunc_i32(d0);
+    y = x86_trunc_i32(d1);
+}
+
+// Camera ray of Renderer::render (renderer.cpp:162-192); 2 jitter draws if spp > 1.
+__device__ __forceinline__ f3 camera_dir(const DevFrame& fr, int pixel, LazyMT& rng) {
+    const CameraConstants& c = fr.cam;
+    const int j = pixel % fr.W, i = pixel / fr.W;
+    const float y = (1.f - (static_cast<float>(i) + 0.5f) * c.invH) * 2.f - 1.f;
+    const float x = ((static_cast<float>(j) + 0.5f) * c.invW) * 2.f - 1.f;
+    float px, py;
+    if (fr.spp == 1) {
+        px = x * c.angle * c.aspect;
+        py = y * c.angle;
+    } else {
+        F2 rs = next2(rng);
+        rs.x -= 0.5f;
+        rs.y -= 0.5f;
+        rs.x = rs.x * c.invW;
+        rs.y = rs.y * c.invH;
+        px = (x + rs.x) * c.angle * c.aspect;
+        py = (y + rs.y) * c.angle;
+    }
+    const float* m = c.c2w;  // cameraToWorld * (px, py, -near, 0)
+    f3 d;
+    d.x = (m[0] * px + m[4] * py) + (m[8] * -1.f + m[12] * 0.f);
+    d.y = (m[1] * px + m[5] * py) + (m[9] * -1.f + m[13] * 0.f);
+    d.z = (m[2] * px + m[6] * py) + (m[10] * -1.f + m[14] * 0.f);
+    return normalize(d);
+}
+
+// --------------------------------------------------------- lane state machine
+enum : uint32_t {  // the query a lane waits on
+    ST_IDLE = 0,
+    ST_PRIMARY,  // render(): primary closest hit (bdpt.h:225)
+    ST_LIGHT,    // lightSubpathWalk closest hit (bdpt.h:190)
+    ST_SPLAT,    // connectToCamera visibility (bdpt.h:318)
+    ST_EYE,      // eyeSubpathWalk closest hit (bdpt.h:70)
+    ST_NEE,      // connectToLight visibility (bdpt.h:405)
+    ST_CONN,     // connectVertices visibility (bdpt.h:451)
+};
+enum : uint32_t {  // actions that need no query
+    A_ISSUED = 0,
+    A_START_LIGHT,
+    A_LIGHT_NEXT,
+    A_LIGHT_VERTEX,
+    A_LIGHT_CONTINUE,
+    A_START_EYE,
+    A_EYE_NEXT,
+    A_EYE_VERTEX,
+    A_CONN,
+    A_EYE_CONTINUE,
+    A_FINISH,
+    A_DONE,
+};
+
+struct Lane {
+    LazyMT rng;
+    int pixel;
+    uint32_t state;
+    Ray ray;     // the pending query
+    f3 cam_d;    // the camera ray direction (the eye walk re-traces it, bdpt.h:59,70)
+    f3 tp;       // subpath throughput
+    float vc, vcm;
+    int depth;
+    int nl;      // stored light vertices
+    int ci;      // next light vertex to connect
+    bool pure;   // isPathPureSpecular
+    int prim_mat;
+    f3 Li;
+    Hit h;       // current subpath vertex
+    f3 pend;     // contribution applied if the pending shadow ray is unoccluded
+    int pend_px;
+    int steps;   // queries issued for the current sample
+};
+
+template <bool COUNT>
+__device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __restrict__ fb, Counts& cnt) {
+    if (COUNT) cnt.c[7] += L.rng.n;
+    // rgb[p] += acc * (1 / spp) (renderer.cpp:202), one sample at a time.
+    if (!(fr.flags & kFlagNoEyeAccum) && (L.Li.x != 0.f || L.Li.y != 0.f || L.Li.z != 0.f)) {
+        const float inv_spp = 1.f / static_cast<float>(fr.spp);
+        float* px = fb + 3 * static_cast<size_t>(L.pixel);
+        atomicAdd(px + 0, L.Li.x * inv_spp);
+        atomicAdd(px + 1, L.Li.y * inv_spp);
+        atomicAdd(px + 2, L.Li.z * inv_spp);
+    }
+    L.state = ST_IDLE;
+}
+
+// Advances a lane from action `act` until it issues its next query or ends its sample.
+template <bool COUNT>
+__device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
+                        const LightStore& ls, Counts& cnt) {
+    const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
+    const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
+    while (act != A_ISSUED && act != A_DONE) {
+        if (COUNT) {
+            cnt.c[10]++;
+            // one wave-level execution per distinct action present among active lanes
+            for (uint32_t a = A_START_LIGHT; a <= A_FINISH; a++)
+                if (__ballot(act == a) && act == a && first_active_lane()) cnt.c[11]++;
+        }
+        switch (act) {
+            case A_START_LIGHT: {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
+                float emitterPdf, areaPdf;
+                f3 nOut, pOut;
+                const EmitterRecord& e = sample_emitter(sc, L.rng, emitterPdf, nOut, pOut, areaPdf);
+                const f3 edir = uniform_hemisphere(next2(L.rng));
+                float emissionPdf = kInvTwoPi * areaPdf;
+                areaPdf *= emitterPdf;
+                emissionPdf *= emitterPdf;
+                f3 fs, ft;
+                make_frame(nOut, fs, ft);
+                L.ray = Ray{pOut, to_world(fs, ft, nOut, edir), kEpsilon, 3.402823466e+38f};
+                L.tp = (ld3(e.radiance) * edir.z) * (1.f / emissionPdf);
+                L.vc = edir.z * (1.f / emissionPdf);
+                L.vcm = areaPdf / emissionPdf;
+                L.nl = 0;
+                L.depth = 1;
+                act = (edir.z <= 0.f) ? A_START_EYE : A_LIGHT_NEXT;
+                break;
+            }
+            case A_LIGHT_NEXT:  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
+                if (!(L.depth < fr.rr_depth)) {
+                    (void)next1(L.rng);
+                    act = A_START_EYE;
+                } else {
+                    L.state = ST_LIGHT;
+                    act = A_ISSUED;
+                }
+                break;
+            case A_LIGHT_VERTEX: {  // bdpt.h:193-209
+                const float dist2 = L.h.dist * L.h.dist;
+                const float absCosIn = fabsf(L.h.wo.z);
+                L.vcm *= (dist2 / absCosIn);
+                L.vc *= (1.f / absCosIn);
+                act = A_LIGHT_CONTINUE;
+                const BsdfRecord& b = sc.bsdf[L.h.mat];
+                if (is_delta(b)) break;
+                // connectToCamera (bdpt.h:295-371): everything but the visibility test.
+                f3 e2l = L.h.p - cam_o;
+                const float invD2 = 1.f / dot(e2l, e2l);
+                e2l = e2l * sqrt_cr(invD2);
+                int xp, yp;
+                splat_pixel(fr.cam, L.h.p, xp, yp);
+                if (xp < 0 || yp < 0 || xp >= fr.W || yp >= fr.H) break;
+                const float cosCamera = dot(fwd, e2l);
+                if (cosCamera <= 0.f) break;
+                const f3 wi = to_local(L.h.s, L.h.t, L.h.n, -e2l);
+                const f3 f = bsdf_eval(b, wi, L.h.wo);
+                if (is_zero(f) || wi.z <= 0.f) break;
+                const float d = fr.cam.vnear / cosCamera;
+                const float img2solid = d * d / cosCamera;
+                const float img2surf = img2solid * (wi.z * invD2);
+                const float surf2img = 1.f / img2surf;
+                const float nlight = static_cast<float>(fr.W * fr.H);
+                f3 rad = L.tp * (f * (1.f / wi.z));
+                rad = rad * (1.f / surf2img);
+                rad = rad * (1.f / nlight);
+                rad = rad * (1.f / static_cast<float>(fr.spp));
+                const float reversePdf_a = 1.f * img2surf;
+                const float prevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;  // swapped (wi, wo), rr = 1
+                const float lightWeight = (reversePdf_a / nlight) * (L.vcm + prevRev * L.vc);
+                const float mis = 1.f / (lightWeight + 1.f + 0.f);
+                L.pend = (fr.strategy == 0) ? rad * mis : rad;
+                L.pend_px = yp * fr.W + xp;
+                L.ray = shadow_ray(cam_o, L.h.p);
+                L.state = ST_SPLAT;
+                act = A_ISSUED;
+                break;
+            }
+            case A_LIGHT_CONTINUE: {  // bdpt.h:211-215
+                const BsdfRecord& b = sc.bsdf[L.h.mat];
+                const bool delta = is_delta(b);
+                if (!delta) store_vertex(ls, L.nl, L.h, L.tp, L.vcm, L.vc, 1.f);  // the pre-walk vertex state
+                if (!continue_walk(b, L.h, L.rng, L.tp, L.depth, L.vc, L.vcm, L.ray)) {
+                    act = A_START_EYE;
+                    break;
+                }
+                if (!delta) {
+                    L.nl++;
+                    if (COUNT) cnt.c[4]++;
+                }
+                act = A_LIGHT_NEXT;
+                break;
+            }
+            case A_START_EYE: {  // eyeSubpathWalk prologue (bdpt.h:47-65)
+                if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
+                    L.Li = ld3(sc.bsdf[L.prim_mat].emission);
+                    act = A_FINISH;
+                    break;
+                }
+                const float cosCamera = dot(fwd, L.cam_d);
+                const float d = fr.cam.vnear / cosCamera;
+                const float t1Pdf = 1.f * (d * d / cosCamera);
+                L.tp = mk(1.f, 1.f, 1.f);
+                L.vc = 0.f;
+                L.vcm = static_cast<float>(fr.W * fr.H) * (1.f / t1Pdf);
+                L.depth = 1;
+                L.pure = true;
+                L.Li = mk(0.f, 0.f, 0.f);
+                L.ray = Ray{cam_o, L.cam_d, 1.f, 1000.f};
+                act = A_EYE_NEXT;
+                break;
+            }
+            case A_EYE_NEXT:  // bdpt.h:68
+                if (!(L.depth < fr.rr_depth)) {
+                    (void)next1(L.rng);
+                    act = A_FINISH;
+                } else {
+                    L.state = ST_EYE;
+                    act = A_ISSUED;
+                }
+                break;
+            case A_EYE_VERTEX: {  // bdpt.h:73-150
+                const float dist2 = L.h.dist * L.h.dist;
+                const float absCosIn = fabsf(L.h.wo.z);
+                L.vcm *= (dist2 / absCosIn);
+                L.vc *= (1.f / absCosIn);
+                const BsdfRecord& b = sc.bsdf[L.h.mat];
+                const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
+                if (!is_zero(emission)) {
+                    const int eid = sc.shape_emitter[L.h.shape];
+                    if (eid >= 0) {  // (the reference asserts otherwise, integrator.cpp:56)
+                        const EmitterRecord& e = sc.emit[eid];
+                        const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
+                        if (L.depth > 1) {
+                            f3 contrib = ld3(e.radiance) * L.tp;
+                            const float pA = 1.f / (e.area * emitterPdf);
+                            const float camW = pA * L.vcm + (pA * kInvTwoPi) * L.vc;
+                            const float mis = 1.f / (1.f + camW);
+                            if (fr.strategy == 2) {  // PATH_TRACING (bdpt.h:110-113)
+                                if (L.pure) L.Li = L.Li + contrib;
+                            } else {
+                                if (!L.pure) contrib = contrib * mis;
+                                L.Li = L.Li + contrib;
+                            }
+                        } else if (L.depth == 1) {
+                            L.Li = L.Li + emission;
+                        }
+                    }
+                    act = A_FINISH;
+                    break;
+                }
+                if (is_delta(b)) {
+                    act = A_EYE_CONTINUE;
+                    break;
+                }
+                L.pure = false;
+                L.ci = 0;
+                act = A_CONN;
+                // connectToLight (bdpt.h:374-430): 4 draws, then everything but visibility.
+                float emitterPdf, posPdf;
+                f3 en, ep;
+                const EmitterRecord& e = sample_emitter(sc, L.rng, emitterPdf, en, ep, posPdf);
+                f3 dir = L.h.p - ep;
+                const float d2 = dot(dir, dir);
+                dir = dir * (1.f / sqrt_cr(d2));
+                const f3 wi = to_local(L.h.s, L.h.t, L.h.n, -dir);
+                const float cosAtLight = dot(en, dir);
+                const float cosAtEye = wi.z;
+                if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
+                const float pdf_w = (emitterPdf * posPdf) * d2 / cosAtLight;
+                const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * (1.f / pdf_w)) * L.tp) * ld3(e.radiance);
+                if (is_zero(Li)) break;
+                const float lightWeight = (bsdf_pdf(b, wi, L.h.wo) * 1.f) / pdf_w;
+                const float eyePrevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;
+                const float eyeCurRev_a = cosAtEye * (1.f / d2) * kInvTwoPi;
+                const float eyeWeight = eyeCurRev_a * (L.vcm + eyePrevRev * L.vc);
+                const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
+                L.pend = (fr.strategy == 0) ? Li * mis : Li;
+                L.ray = shadow_ray(L.h.p, ep);
+                L.state = ST_NEE;
+                act = A_ISSUED;
+                break;
+            }
+            case A_CONN: {  // connectVertices (bdpt.h:434-483) with light vertex ci
+                act = A_EYE_CONTINUE;
+                if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
+                const BsdfRecord& be = sc.bsdf[L.h.mat];
+                while (L.ci < L.nl) {
+                    const Vertex V = load_vertex(ls, L.ci);
+                    if (COUNT) cnt.c[5]++;
+                    f3 dir = L.h.p - V.p;
+                    const float invD2 = 1.f / dot(dir, dir);
+                    dir = dir * sqrt_cr(invD2);
+                    const f3 wiL = to_local(V.s, V.t, V.n, dir);
+                    const f3 wiE = to_local(L.h.s, L.h.t, L.h.n, -dir);
+                    const float cosL = wiL.z, cosE = wiE.z;
+                    if (cosL <= 0.f || cosE <= 0.f) {
+                        L.ci++;
+                        continue;
+                    }
+                    const BsdfRecord& bl = sc.bsdf[V.mat];
+                    f3 Li = bsdf_eval(bl, wiL, V.wo) * bsdf_eval(be, wiE, L.h.wo);
+                    Li = Li * ((V.tp * L.tp) * invD2);
+                    const float eyePathRev_w = bsdf_pdf(bl, wiL, V.wo) * V.rr;
+                    const float lightPrevRev = bsdf_pdf(bl, V.wo, wiL) * V.rr;
+                    const float lightPathRev_w = bsdf_pdf(be, wiE, L.h.wo) * 1.f;
+                    const float eyePrevRev = bsdf_pdf(be, L.h.wo, wiE) * 1.f;
+                    const float lightPathRev_a = lightPathRev_w * cosL * invD2;
+                    const float eyePathRev_a = eyePathRev_w * cosE * invD2;
+                    const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
+                    const float eyeWeight = eyePathRev_a * (L.vcm + eyePrevRev * L.vc);
+                    const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
+                    L.pend = Li * mis;
+                    L.ray = shadow_ray(L.h.p, V.p);
+                    L.state = ST_CONN;
+                    act = A_ISSUED;
+                    break;
+                }
+                break;
+            }
+            case A_EYE_CONTINUE:  // bdpt.h:152
+                act = continue_walk(sc.bsdf[L.h.mat], L.h, L.rng, L.tp, L.depth, L.vc, L.vcm, L.ray) ? A_EYE_NEXT
+                                                                                                       : A_FINISH;
+                break;
+            case A_FINISH:
+                finish<COUNT>(L, fr, fb, cnt);
+                act = A_DONE;
+                break;
+            default:
+                act = A_DONE;
+        }
+    }
+}
+
+// Starts sample `s` of the shard on this lane: seed, camera ray, primary query.
+__device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame& fr) {
+    const uint64_t per_row = static_cast<uint64_t>(fr.W) * fr.spp;
+    const uint64_t lr = s / per_row, q = s % per_row;
+    const int j = static_cast<int>(q / fr.spp), k = static_cast<int>(q % fr.spp);
+    const int row = fr.row_offset + static_cast<int>(lr) * fr.row_stride;
+    L.pixel = row * fr.W + j;
+    mt_seed(L.rng, fr.seed_base + static_cast<uint32_t>(L.pixel) * static_cast<uint32_t>(fr.spp) +
+                       static_cast<uint32_t>(k));
+    L.cam_d = camera_dir(fr, L.pixel, L.rng);
+    L.ray = Ray{mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]), L.cam_d, 1.f, 1000.f};
+    L.Li = mk(0.f, 0.f, 0.f);
+    L.steps = 0;
+    L.state = ST_PRIMARY;
+}
+
+__device__ __forceinline__ bool is_shadow_state(uint32_t st) { return st == ST_SPLAT || st == ST_NEE || st == ST_CONN; }
+
+// Applies the result of the lane's pending query (closest hit: leaf-order
+// triangle index res >= 0 with t, u, v; shadow ray: res >= 0 = occluded) and
+// returns the action the state machine continues with.
+template <bool COUNT>
+__device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, float v, const DevScene& sc,
+                                            const DevFrame& fr, float* __restrict__ fb, Counts& cnt) {
+    const bool any = is_shadow_state(L.state);
+    bool hit = res >= 0;
+    if (hit && !any) hit = (t <= L.ray.max_t && t >= L.ray.min_t);  // accel.h:133
+    if (hit && !any) shade_hit(sc, res, u, v, t, L.ray.d, L.h);
+    uint32_t act;
+    switch (L.state) {
+        case ST_PRIMARY:
+            if (!hit) act = A_FINISH;
+            else {
+                L.prim_mat = L.h.mat;
+                act = (fr.strategy == 2) ? A_START_EYE : A_START_LIGHT;
+            }
+            break;
+        case ST_LIGHT: act = hit ? A_LIGHT_VERTEX : A_START_EYE; break;
+        case ST_SPLAT:
+            if (!hit) {
+                if (COUNT) cnt.c[6]++;
+                float* px = fb + 3 * static_cast<size_t>(L.pend_px);
+                atomicAdd(px + 0, L.pend.x);
+                atomicAdd(px + 1, L.pend.y);
+                atomicAdd(px + 2, L.pend.z);
+            }
+            act = A_LIGHT_CONTINUE;
+            break;
+        case ST_EYE: act = hit ? A_EYE_VERTEX : A_FINISH; break;
+        case ST_NEE:
+            if (!hit) L.Li = L.Li + L.pend;
+            act = A_CONN;
+            break;
+        case ST_CONN:
+            if (!hit) L.Li = L.Li + L.pend;
+            L.ci++;
+            act = A_CONN;
+            break;
+        default: act = A_DONE;
+    }
+    // A state-machine bug must not hang the GPU: bound the queries per sample.
+    if (++L.steps > kMaxStepsPerSample && act != A_FINISH) act = A_FINISH;
+    return act;
+}
+
+__device__ __forceinline__ void flush_counts(const Counts& cnt, unsigned long long* out) {
+    for (int i = 0; i < kCounters; i++) {
+        unsigned long long v = cnt.c[i];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(out + i, v);
+    }
+}
+
+}  // namespace dev
+}  // namespace bdpt

@@ -54,6 +54,7 @@ extern "C" {
 /* bdpt_frame_params.flags */
 #define BDPT_FLAG_COUNT 1u            /* counting pass: fill bdpt_stats.counters (slower) */
 #define BDPT_FLAG_FULL_TRAVERSAL 2u   /* visit every box the reference visits (no t-culling) */
+#define BDPT_FLAG_WAVEFRONT 4u        /* wavefront passes (shade / trace kernels) instead of the megakernel */
 
 typedef struct bdpt_scene bdpt_scene; /* host-side ingested scene */
 typedef struct bdpt_ctx bdpt_ctx;     /* device context (one HIP device) */

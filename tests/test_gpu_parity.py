@@ -53,11 +53,12 @@ def report(fb, ref):
     return e.max(), exact, whole
 
 
+@pytest.mark.parametrize("sched", [0, bdpt_amd.FLAG_WAVEFRONT], ids=["megakernel", "wavefront"])
 @pytest.mark.parametrize("name", FB_CASES)
-def test_gpu_matches_reference_golden(name, golden_manifest):
+def test_gpu_matches_reference_golden(name, sched, golden_manifest):
     m = golden_manifest["framebuffers"][name]
     it = integrator(m["scene"], m["width"], m["height"], m["spp"], m["rr_depth"])
-    fb = it.render_frame(row_offset=0, row_stride=m["row_stride"]).reshape(-1)
+    fb = it.render_frame(row_offset=0, row_stride=m["row_stride"], flags=sched).reshape(-1)
     assert it.stats()["samples"] == m["samples"]
     ref = load_golden(name)
     worst, exact, whole = report(fb, ref)
@@ -65,12 +66,14 @@ def test_gpu_matches_reference_golden(name, golden_manifest):
     assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact floats {exact:.4f}, image {whole:.3g})"
 
 
-def test_gpu_full_traversal_equals_culled_traversal():
-    """Distance culling + near-first order must not change any closest hit."""
+@pytest.mark.parametrize("sched", [0, bdpt_amd.FLAG_WAVEFRONT])
+def test_gpu_full_traversal_equals_culled_traversal(sched):
+    """The reference's own binary tree walked without culling (FULL) and the
+    4-wide hierarchy with distance culling give the same closest hits."""
     a = integrator("caustic", 64, 64, 16, 8)
-    fa = a.render_frame().copy()
+    fa = a.render_frame(flags=sched).copy()
     b = integrator("caustic", 64, 64, 16, 8)
-    fb = b.render_frame(flags=bdpt_amd.FLAG_FULL_TRAVERSAL).copy()
+    fb = b.render_frame(flags=bdpt_amd.FLAG_FULL_TRAVERSAL | sched).copy()
     assert rel_l2(fa, fb).max() <= TOL
 
 
@@ -179,3 +182,21 @@ def test_gpu_full_size_caustic_properties(golden_manifest):
     assert np.all(np.abs(mean - ref_mean) / ref_mean < 0.03), (mean, ref_mean)
     it2 = integrator("caustic", 512, 512, 16, 8)
     assert rel_l2(it2.render_frame(), fb).max() <= TOL
+
+
+@pytest.mark.parametrize("slots", ["256", "1000", "4096"])
+def test_gpu_wavefront_slot_pool_refills(slots, monkeypatch):
+    """Few path slots: every slot renders many samples in turn (partitioned
+    sample counters, slot chunks smaller than a wave) — same image as the oracle."""
+    monkeypatch.setenv("BDPT_WF_SLOTS", slots)
+    name, W, H, spp, rr = "caustic", 40, 24, 5, 8
+    fb = integrator(name, W, H, spp, rr).render_frame(flags=bdpt_amd.FLAG_WAVEFRONT).reshape(-1)
+    ref, _ = O.Scene(variants.obj_path(name)).render(O.make_params(variants.SCENES[name]["camera"], W, H, spp, rr))
+    worst, exact, _ = report(fb, ref)
+    assert worst <= TOL, f"slots={slots}: max per-pixel rel L2 {worst:.3g}"
+
+
+def test_gpu_megakernel_matches_wavefront():
+    a = integrator("hardlight_mirror", 48, 40, 6, 5).render_frame().copy()
+    b = integrator("hardlight_mirror", 48, 40, 6, 5).render_frame(flags=bdpt_amd.FLAG_WAVEFRONT).copy()
+    assert rel_l2(a, b).max() <= TOL

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Builds a kernel variant of the product library: tools/build_variant.sh NAME [hipcc flags...]
+# Builds a kernel variant of the product library: tools/build_variant.sh NAME [hipcc -D flags...]
 # -> bidirectional-path-tracing_amd/lib/libbdpt_amd_NAME.so (select with BDPT_AMD_LIB=...).
 set -e
 cd "$(dirname "$0")/../bidirectional-path-tracing_amd"
@@ -7,6 +7,8 @@ NAME=$1; shift
 O=lib/obj_$NAME
 mkdir -p $O
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I../include -Icsrc"
-/opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/bdpt_kernels.hip -o $O/k.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $O/k.o lib/obj/bdpt_capi.o lib/obj/scene.o lib/obj/wide_bvh.o -o lib/libbdpt_amd_$NAME.so
+/opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/bdpt_kernels.hip -o $O/k.o &
+/opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/bdpt_wavefront.hip -o $O/w.o &
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $O/k.o $O/w.o lib/obj/bdpt_capi.o lib/obj/scene.o lib/obj/wide_bvh.o -o lib/libbdpt_amd_$NAME.so
 echo lib/libbdpt_amd_$NAME.so

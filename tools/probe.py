@@ -15,9 +15,17 @@ sc = variants.SCENES[name]
 cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**sc["camera"]), width=W, height=H, spp=spp, rr_depth=sc["rr_depth"])
 it = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(name)), cfg)
 it.init()
-it.render_frame()
+xf = int(os.environ.get("PROBE_FLAGS", "0"))  # e.g. 4 = wavefront schedule
+it.render_frame(flags=xf)
+it.render_frame(flags=xf)
 t_plain = it.stats()["kernel_ms"]
-it.render_frame(flags=bdpt_amd.FLAG_COUNT)
+launches = it.stats()["launches"]
+if os.environ.get("PROBE_QUICK"):
+    n = it.stats()["samples"]
+    print(json.dumps({"scene": name, "W": W, "H": H, "spp": spp, "kernel_ms": round(t_plain, 3), "launches": launches,
+                      "msamples_per_s": round(n / t_plain * 1e-3, 3)}))
+    sys.exit(0)
+it.render_frame(flags=bdpt_amd.FLAG_COUNT | xf)
 st = it.stats()
 c, n = st["counters"], st["samples"]
 out = {k: round(v / n, 3) for k, v in c.items()}
@@ -27,5 +35,6 @@ lc = max(c["loop_clocks"], 1)
 out["trav_clock_frac"] = round(c["trav_clocks"] / lc, 4)
 out["shade_clock_frac"] = round(c["shade_clocks"] / lc, 4)
 out["kernel_ms"] = round(t_plain, 3)
+out["launches"] = launches
 out["msamples_per_s"] = round(n / t_plain * 1e-3, 3)
 print(json.dumps({"scene": name, "W": W, "H": H, "spp": spp, **out}))
