@@ -35,9 +35,9 @@ hipError_t wf_set_params(const dev::DevScene& sc, const dev::DevFrame& fr, float
                          unsigned long long* counters, uint32_t* sstack, uint32_t nslots, uint32_t trace_lanes,
                          int shade_lds, void* dparams, hipStream_t stream);
 hipError_t wf_launch_pass(const void* dparams, uint32_t flags, uint32_t nslots, int trace_grid, int shade_lds,
-                          int64_t pass, hipStream_t stream);
+                          uint32_t p_lds_words, int64_t pass, hipStream_t stream);
 int wf_parts();
-int frame_kernel_blocks_per_cu();
+int frame_kernel_blocks_per_cu(size_t dyn_lds);
 int frame_kernel_block();
 int light_vertex_fields();
 }  // namespace bdpt
@@ -266,6 +266,17 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     c->sc.shape_emitter = static_cast<const int32_t*>(p);
     c->sc.root_link = L.root_link;
     c->sc.nemit = static_cast<int32_t>(L.emitters.size());
+    c->sc.nbsdf = static_cast<int32_t>(L.bsdfs.size());
+    c->sc.nshapes = static_cast<int32_t>(L.shape_emitter.size());
+    {  // LDS table layout (bdpt_device.hpp scene_tables_to_lds), 16-byte aligned parts
+        auto up4 = [](uint32_t w) { return (w + 3u) & ~3u; };
+        const uint32_t nb = static_cast<uint32_t>(L.bsdfs.size() * sizeof(BsdfRecord) / 4);
+        c->sc.lds_emit_off = up4(nb);
+        c->sc.lds_shape_off = up4(c->sc.lds_emit_off + static_cast<uint32_t>(L.emitters.size() * sizeof(EmitterRecord) / 4));
+        c->sc.lds_words = up4(c->sc.lds_shape_off + static_cast<uint32_t>(L.shape_emitter.size()));
+        if (c->sc.lds_words * 4u > 24u * 1024u)
+            return fail(BDPT_ERR_UNSUPPORTED, "BSDF / emitter / shape tables exceed the 24 KiB LDS budget");
+    }
     c->max_depth = s->host.max_depth;
     HIP_TRY(hipMalloc(&c->work, sizeof(unsigned long long)));
     HIP_TRY(hipMalloc(&c->counters, sizeof(unsigned long long) * BDPT_NUM_COUNTERS));
@@ -273,7 +284,7 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     HIP_TRY(hipMalloc(&c->dparams, frame_params_bytes()));
     // Persistent grid: exactly the resident blocks (no co-residency is assumed:
     // the work queue has no inter-block waits, extra blocks would just queue).
-    c->grid = c->cus * frame_kernel_blocks_per_cu();
+    c->grid = c->cus * frame_kernel_blocks_per_cu(4 * static_cast<size_t>(c->sc.lds_words));
     c->nslots = static_cast<uint32_t>(c->grid * frame_kernel_block());
     // Traversal stack: worst case of either tree (binary: depth + 1 pending
     // right children; 4-wide: the host-computed bound), the part beyond the
@@ -383,7 +394,8 @@ static int render_wavefront(bdpt_ctx* c, const dev::DevFrame& fr, float* fb, hip
     int64_t k = 0;
     for (int64_t chunk = 0;; chunk++) {
         for (int j = 0; j < kChunk; j++, k++)
-            HIP_TRY(wf_launch_pass(c->wf_dparams, fr.flags, nslots, c->trace_grid, c->shade_lds, k, st));
+            HIP_TRY(wf_launch_pass(c->wf_dparams, fr.flags, nslots, c->trace_grid, c->shade_lds, c->sc.lds_words, k,
+                                   st));
         uint32_t* hc = c->host_ctr + 320 * (chunk & 1);
         HIP_TRY(hipMemcpyAsync(hc, c->wf_tctr, 320 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipEventRecord(c->chunk_ev[chunk & 1], st));

@@ -18,6 +18,9 @@ constexpr float kInvTwoPi = 0.15915494309189533577f;  // platform.h:52
 constexpr float kEpsilon = 1e-8f;                     // platform.h:56
 constexpr float kTriMinT = 0x1.0624dep-10f;           // smallest float t with (double)t > 1e-3 (accel.h:43)
 constexpr int kCounters = 16;
+#ifndef BDPT_TRAV_WHILE_WHILE
+#define BDPT_TRAV_WHILE_WHILE 1  // megakernel traversal loop shape (0: one node or leaf per iteration)
+#endif
 
 // ------------------------------------------------------------------ inputs
 // Loads through an address-space-1 pointer compile to global_load (SGPR/VGPR
@@ -45,8 +48,41 @@ struct DevScene {
     const float* __restrict__ emit_cdf;
     const int32_t* __restrict__ shape_emitter;
     uint32_t root_link, wroot_link;
-    int32_t nemit;
+    int32_t nemit, nbsdf, nshapes;
+    // LDS copy of the small tables (scene_tables_to_lds): word offsets of the
+    // emitter records and the shape->emitter map, total words (16-byte rounded)
+    uint32_t lds_emit_off, lds_shape_off, lds_words;
 };
+
+// Small per-scene tables — BSDF records, emitter records, shape -> emitter
+// map — live in the kernels' dynamic LDS: the divergent shading code reads
+// them with ds_read instead of chains of dependent global loads. Layout (words):
+// [0, emit_off) BsdfRecord[nbsdf], [emit_off, shape_off) EmitterRecord[nemit],
+// [shape_off, ...) int32 shape_emitter[nshapes]; anything a kernel keeps in
+// dynamic LDS besides goes at lds_words.
+extern __shared__ uint32_t g_scene_lds[];
+__device__ __forceinline__ const BsdfRecord& bsdf_of(const DevScene&, int m) {
+    return reinterpret_cast<const BsdfRecord*>(g_scene_lds)[m];
+}
+__device__ __forceinline__ const EmitterRecord& emitter_of(const DevScene& sc, int i) {
+    return reinterpret_cast<const EmitterRecord*>(g_scene_lds + sc.lds_emit_off)[i];
+}
+__device__ __forceinline__ int shape_emitter_of(const DevScene& sc, int shape) {
+    return static_cast<int>(g_scene_lds[sc.lds_shape_off + shape]);
+}
+// Cooperative copy by the whole block, then a barrier.
+__device__ __forceinline__ void scene_tables_to_lds(const DevScene& sc) {
+    const uint32_t nb = static_cast<uint32_t>(sc.nbsdf) * (sizeof(BsdfRecord) / 4);
+    const uint32_t ne = static_cast<uint32_t>(sc.nemit) * (sizeof(EmitterRecord) / 4);
+    const uint32_t* b = reinterpret_cast<const uint32_t*>(sc.bsdf);
+    const uint32_t* e = reinterpret_cast<const uint32_t*>(sc.emit);
+    const uint32_t* m = reinterpret_cast<const uint32_t*>(sc.shape_emitter);
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) g_scene_lds[i] = b[i];
+    for (uint32_t i = threadIdx.x; i < ne; i += blockDim.x) g_scene_lds[sc.lds_emit_off + i] = e[i];
+    for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(sc.nshapes); i += blockDim.x)
+        g_scene_lds[sc.lds_shape_off + i] = m[i];
+    __syncthreads();
+}
 
 struct DevFrame {
     CameraConstants cam;
@@ -463,6 +499,70 @@ __device__ __forceinline__ TravState trav_begin(const DevScene& sc, const Ray& r
     return TravState{sc.wroot_link, 0, -1, r.max_t, 0.f, 0.f};
 }
 
+// Pops the nearest pending entry that can still hold a closer hit; false when
+// the traversal is complete.
+__device__ __forceinline__ bool trav_pop(const Ray& r, bool any, TravState& ts, const Stack& stk) {
+    while (ts.sp > 0) {
+        const uint2 e = stk.get(--ts.sp);
+        if (!(__uint_as_float(e.y) > cull_far(any ? r.max_t : ts.best_t))) {
+            ts.link = e.x;
+            return true;
+        }
+    }
+    return false;
+}
+
+// Interior 4-wide node ts.link: tests the four children, descends into the
+// nearest hit child (true) and stacks the others far-to-near; false when no
+// child is hit (the caller pops).
+template <bool COUNT>
+__device__ __forceinline__ bool trav_node(const DevScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
+                                          const Stack& stk, Counts& cnt) {
+    if (COUNT) cnt.c[2]++;
+    const float4* nd = sc.wnodes + 8 * static_cast<size_t>(ts.link);
+    const float4 lx = gld4(nd), hx = gld4(nd + 1), ly = gld4(nd + 2), hy = gld4(nd + 3), lz = gld4(nd + 4),
+                 hz = gld4(nd + 5), lk = gld4(nd + 6);
+    const float far = cull_far(any ? r.max_t : ts.best_t);
+    float key[4];
+    uint32_t lnk[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const float clx = (&lx.x)[c], chx = (&hx.x)[c], cly = (&ly.x)[c], chy = (&hy.x)[c], clz = (&lz.x)[c],
+                    chz = (&hz.x)[c];
+        const uint32_t l = __float_as_uint((&lk.x)[c]);
+        float tn, tf;
+        int d = slab_fast(clx, cly, clz, chx, chy, chz, r.o, ri.inv, tn, tf);
+        const bool leaf = (l & kLeafBit) != 0 && l != kEmptyLinkDev;
+        if (d == kSlabAmbiguous && leaf) {
+            d = slab_cross(clx, cly, clz, chx, chy, chz, r.o, ri.inv);
+            if (d == kSlabAmbiguous) {
+                if (COUNT) cnt.c[15]++;
+                float en, ex;
+                d = slab(clx, cly, clz, chx, chy, chz, r, en, ex) ? kSlabHit : kSlabMiss;
+            }
+        }
+        const bool hit = l != kEmptyLinkDev && d != kSlabMiss && !(tn > far) && !(tf < kCullNear);
+        key[c] = hit ? tn : __builtin_inff();
+        lnk[c] = hit ? l : kEmptyLinkDev;
+    }
+    // near-first order: sorting network on (key, link)
+#define BDPT_CE(a, b)                                                       \
+    {                                                                       \
+        const bool sw = key[b] < key[a];                                    \
+        const float k0 = sw ? key[b] : key[a], k1 = sw ? key[a] : key[b];   \
+        const uint32_t l0 = sw ? lnk[b] : lnk[a], l1 = sw ? lnk[a] : lnk[b]; \
+        key[a] = k0, key[b] = k1, lnk[a] = l0, lnk[b] = l1;                 \
+    }
+    BDPT_CE(0, 1) BDPT_CE(2, 3) BDPT_CE(0, 2) BDPT_CE(1, 3) BDPT_CE(1, 2)
+#undef BDPT_CE
+    if (lnk[0] == kEmptyLinkDev) return false;
+    if (lnk[3] != kEmptyLinkDev) stk.put(ts.sp++, lnk[3], key[3]);
+    if (lnk[2] != kEmptyLinkDev) stk.put(ts.sp++, lnk[2], key[2]);
+    if (lnk[1] != kEmptyLinkDev) stk.put(ts.sp++, lnk[1], key[1]);
+    ts.link = lnk[0];
+    return true;
+}
+
 // One loop iteration (a 4-wide node or a leaf, then the pop). Returns true
 // when the query is complete (result in ts.best / best_t / best_u / best_v).
 template <bool COUNT>
@@ -472,64 +572,40 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, const Ray& r, cons
         cnt.c[8]++;
         if (first_active_lane()) cnt.c[9]++;
     }
-    const uint32_t link = ts.link;
-    if (link & kLeafBit) {
-        if (leaf_tests<COUNT>(sc, link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return true;
-    } else {
-        if (COUNT) cnt.c[2]++;
-        const float4* nd = sc.wnodes + 8 * static_cast<size_t>(link);
-        const float4 lx = gld4(nd), hx = gld4(nd + 1), ly = gld4(nd + 2), hy = gld4(nd + 3), lz = gld4(nd + 4),
-                     hz = gld4(nd + 5), lk = gld4(nd + 6);
-        const float far = cull_far(any ? r.max_t : ts.best_t);
-        float key[4];
-        uint32_t lnk[4];
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const float clx = (&lx.x)[c], chx = (&hx.x)[c], cly = (&ly.x)[c], chy = (&hy.x)[c], clz = (&lz.x)[c],
-                        chz = (&hz.x)[c];
-            const uint32_t l = __float_as_uint((&lk.x)[c]);
-            float tn, tf;
-            int d = slab_fast(clx, cly, clz, chx, chy, chz, r.o, ri.inv, tn, tf);
-            const bool leaf = (l & kLeafBit) != 0 && l != kEmptyLinkDev;
-            if (d == kSlabAmbiguous && leaf) {
-                d = slab_cross(clx, cly, clz, chx, chy, chz, r.o, ri.inv);
-                if (d == kSlabAmbiguous) {
-                    if (COUNT) cnt.c[15]++;
-                    float en, ex;
-                    d = slab(clx, cly, clz, chx, chy, chz, r, en, ex) ? kSlabHit : kSlabMiss;
-                }
+    if (ts.link & kLeafBit) {
+        if (leaf_tests<COUNT>(sc, ts.link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return true;
+    } else if (trav_node<COUNT>(sc, r, ri, any, ts, stk, cnt)) {
+        return false;
+    }
+    return !trav_pop(r, any, ts, stk);
+}
+
+// The same walk as a while-while loop (Aila & Laine 2009): lanes descend
+// through interior nodes together until each holds a leaf (or is done), then
+// the leaves are tested together — a wave iteration runs one kind of work.
+template <bool COUNT>
+__device__ __forceinline__ void trav_while_while(const DevScene& sc, const Ray& r, const RayInv& ri, bool any,
+                                                 TravState& ts, const Stack& stk, Counts& cnt) {
+    for (;;) {
+        bool live = true;
+        while (!(ts.link & kLeafBit)) {
+            if (COUNT) {
+                cnt.c[8]++;
+                if (first_active_lane()) cnt.c[9]++;
             }
-            const bool hit = l != kEmptyLinkDev && d != kSlabMiss && !(tn > far) && !(tf < kCullNear);
-            key[c] = hit ? tn : __builtin_inff();
-            lnk[c] = hit ? l : kEmptyLinkDev;
+            if (!trav_node<COUNT>(sc, r, ri, any, ts, stk, cnt) && !trav_pop(r, any, ts, stk)) {
+                live = false;
+                break;
+            }
         }
-        // near-first order: sorting network on (key, link)
-#define BDPT_CE(a, b)                                                       \
-    {                                                                       \
-        const bool sw = key[b] < key[a];                                    \
-        const float k0 = sw ? key[b] : key[a], k1 = sw ? key[a] : key[b];   \
-        const uint32_t l0 = sw ? lnk[b] : lnk[a], l1 = sw ? lnk[a] : lnk[b]; \
-        key[a] = k0, key[b] = k1, lnk[a] = l0, lnk[b] = l1;                 \
-    }
-        BDPT_CE(0, 1) BDPT_CE(2, 3) BDPT_CE(0, 2) BDPT_CE(1, 3) BDPT_CE(1, 2)
-#undef BDPT_CE
-        if (lnk[0] != kEmptyLinkDev) {
-            if (lnk[3] != kEmptyLinkDev) stk.put(ts.sp++, lnk[3], key[3]);
-            if (lnk[2] != kEmptyLinkDev) stk.put(ts.sp++, lnk[2], key[2]);
-            if (lnk[1] != kEmptyLinkDev) stk.put(ts.sp++, lnk[1], key[1]);
-            ts.link = lnk[0];
-            return false;
+        if (!live) return;
+        if (COUNT) {
+            cnt.c[8]++;
+            if (first_active_lane()) cnt.c[9]++;
         }
+        if (leaf_tests<COUNT>(sc, ts.link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return;
+        if (!trav_pop(r, any, ts, stk)) return;
     }
-    // pop the nearest pending entry that can still hold a closer hit
-    while (ts.sp > 0) {
-        const uint2 e = stk.get(--ts.sp);
-        if (!(__uint_as_float(e.y) > cull_far(any ? r.max_t : ts.best_t))) {
-            ts.link = e.x;
-            return false;
-        }
-    }
-    return true;
 }
 
 template <bool FULL, bool COUNT>
@@ -544,8 +620,12 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool a
         return q.best;
     }
     TravState ts = trav_begin(sc, r);
+#if BDPT_TRAV_WHILE_WHILE
+    trav_while_while<COUNT>(sc, r, ri, any, ts, stk, cnt);
+#else
     while (!trav_step<COUNT>(sc, r, ri, any, ts, stk, cnt)) {
     }
+#endif
     bt = ts.best_t, bu = ts.best_u, bv = ts.best_v;
     return ts.best;
 }
@@ -732,7 +812,7 @@ __device__ __forceinline__ const EmitterRecord& sample_emitter(const DevScene& s
     uint32_t id = static_cast<uint32_t>(u0 * static_cast<float>(sc.nemit));
     id = id < static_cast<uint32_t>(sc.nemit - 1) ? id : static_cast<uint32_t>(sc.nemit - 1);
     emitter_pdf = 1.f / static_cast<float>(sc.nemit);
-    const EmitterRecord& e = sc.emit[id];
+    const EmitterRecord& e = emitter_of(sc, static_cast<int>(id));
     const int f = cdf_sample(sc.emit_cdf + e.cdf_offset, e.nfaces + 1, next1(rng));
     const F2 uv = uniform_triangle(next2(rng));
     const float4* q = sc.emit_tri + 5 * static_cast<size_t>(e.face_offset + f);

@@ -68,6 +68,7 @@ template <bool FULL, bool COUNT>
 __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(const KParams* __restrict__ kpp) {
     const KParams& kp = *kpp;
     __shared__ uint2 stack_mem[kLdsStack * kBlock];
+    scene_tables_to_lds(kp.sc);
     const int lane = threadIdx.x & 63;
     const Stack stk{stack_mem + threadIdx.x, kBlock, kLdsStack, kp.gstack, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
     Counts cnt;
@@ -115,6 +116,7 @@ __global__ __launch_bounds__(64) void bdpt_sample_kernel(DevScene sc, DevFrame f
                                                          Ray ray, uint32_t seed, uint32_t draws,
                                                          float* __restrict__ out) {
     __shared__ uint2 stack_mem[kLdsStack * 64];
+    scene_tables_to_lds(sc);
     if (threadIdx.x != 0) return;
     Counts cnt;
     const LightStore ls = light_store(lvbuf, fr.rr_depth, 0);
@@ -150,24 +152,26 @@ hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float*
     if (e != hipSuccess) return e;
     const dev::KParams* kp = static_cast<const dev::KParams*>(dparams);
     const dim3 g(grid), b(dev::kBlock);
-    if (full && count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, true>), g, b, 0, stream, kp);
-    else if (full) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, false>), g, b, 0, stream, kp);
-    else if (count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, true>), g, b, 0, stream, kp);
-    else hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, false>), g, b, 0, stream, kp);
+    const size_t lds = 4 * static_cast<size_t>(sc.lds_words);
+    if (full && count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, true>), g, b, lds, stream, kp);
+    else if (full) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, false>), g, b, lds, stream, kp);
+    else if (count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, true>), g, b, lds, stream, kp);
+    else hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, false>), g, b, lds, stream, kp);
     return hipGetLastError();
 }
 
 hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
                          const dev::Ray& ray, uint32_t seed, uint32_t draws, float* out, hipStream_t stream) {
-    hipLaunchKernelGGL(dev::bdpt_sample_kernel, dim3(1), dim3(64), 0, stream, sc, fr, fb, lvbuf, gstack, ray, seed,
+    hipLaunchKernelGGL(dev::bdpt_sample_kernel, dim3(1), dim3(64), 4 * static_cast<size_t>(sc.lds_words), stream, sc,
+                       fr, fb, lvbuf, gstack, ray, seed,
                        draws, out);
     return hipGetLastError();
 }
 
 // Resident 256-lane blocks per CU for the frame kernel (VGPR and LDS limited).
-int frame_kernel_blocks_per_cu() {
+int frame_kernel_blocks_per_cu(size_t dyn_lds) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::bdpt_frame_kernel<false, false>, dev::kBlock, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::bdpt_frame_kernel<false, false>, dev::kBlock, dyn_lds) !=
             hipSuccess ||
         n <= 0)
         n = BDPT_WAVES_PER_EU;

@@ -242,7 +242,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 L.vcm *= (dist2 / absCosIn);
                 L.vc *= (1.f / absCosIn);
                 act = A_LIGHT_CONTINUE;
-                const BsdfRecord& b = sc.bsdf[L.h.mat];
+                const BsdfRecord& b = bsdf_of(sc, L.h.mat);
                 if (is_delta(b)) break;
                 // connectToCamera (bdpt.h:295-371): everything but the visibility test.
                 f3 e2l = L.h.p - cam_o;
@@ -277,7 +277,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 break;
             }
             case A_LIGHT_CONTINUE: {  // bdpt.h:211-215
-                const BsdfRecord& b = sc.bsdf[L.h.mat];
+                const BsdfRecord& b = bsdf_of(sc, L.h.mat);
                 const bool delta = is_delta(b);
                 if (!delta) store_vertex(ls, L.nl, L.h, L.tp, L.vcm, L.vc, 1.f);  // the pre-walk vertex state
                 if (!continue_walk(b, L.h, L.rng, L.tp, L.depth, L.vc, L.vcm, L.ray)) {
@@ -293,7 +293,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             }
             case A_START_EYE: {  // eyeSubpathWalk prologue (bdpt.h:47-65)
                 if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
-                    L.Li = ld3(sc.bsdf[L.prim_mat].emission);
+                    L.Li = ld3(bsdf_of(sc, L.prim_mat).emission);
                     act = A_FINISH;
                     break;
                 }
@@ -324,12 +324,12 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 const float absCosIn = fabsf(L.h.wo.z);
                 L.vcm *= (dist2 / absCosIn);
                 L.vc *= (1.f / absCosIn);
-                const BsdfRecord& b = sc.bsdf[L.h.mat];
+                const BsdfRecord& b = bsdf_of(sc, L.h.mat);
                 const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
                 if (!is_zero(emission)) {
-                    const int eid = sc.shape_emitter[L.h.shape];
+                    const int eid = shape_emitter_of(sc, L.h.shape);
                     if (eid >= 0) {  // (the reference asserts otherwise, integrator.cpp:56)
-                        const EmitterRecord& e = sc.emit[eid];
+                        const EmitterRecord& e = emitter_of(sc, eid);
                         const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
                         if (L.depth > 1) {
                             f3 contrib = ld3(e.radiance) * L.tp;
@@ -384,7 +384,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             case A_CONN: {  // connectVertices (bdpt.h:434-483) with light vertex ci
                 act = A_EYE_CONTINUE;
                 if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
-                const BsdfRecord& be = sc.bsdf[L.h.mat];
+                const BsdfRecord& be = bsdf_of(sc, L.h.mat);
                 while (L.ci < L.nl) {
                     const Vertex V = load_vertex(ls, L.ci);
                     if (COUNT) cnt.c[5]++;
@@ -398,7 +398,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                         L.ci++;
                         continue;
                     }
-                    const BsdfRecord& bl = sc.bsdf[V.mat];
+                    const BsdfRecord& bl = bsdf_of(sc, V.mat);
                     f3 Li = bsdf_eval(bl, wiL, V.wo) * bsdf_eval(be, wiE, L.h.wo);
                     Li = Li * ((V.tp * L.tp) * invD2);
                     const float eyePathRev_w = bsdf_pdf(bl, wiL, V.wo) * V.rr;
@@ -419,7 +419,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 break;
             }
             case A_EYE_CONTINUE:  // bdpt.h:152
-                act = continue_walk(sc.bsdf[L.h.mat], L.h, L.rng, L.tp, L.depth, L.vc, L.vcm, L.ray) ? A_EYE_NEXT
+                act = continue_walk(bsdf_of(sc, L.h.mat), L.h, L.rng, L.tp, L.depth, L.vc, L.vcm, L.ray) ? A_EYE_NEXT
                                                                                                        : A_FINISH;
                 break;
             case A_FINISH:

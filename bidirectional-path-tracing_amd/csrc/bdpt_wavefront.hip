@@ -188,7 +188,8 @@ __device__ __forceinline__ uint64_t claim_samples(bool want, const WfParams& P, 
 template <bool FULL, bool COUNT>
 __global__ __launch_bounds__(kShadeBlock) void bdpt_shade_kernel(const WfParams* __restrict__ pp, int parity) {
     const WfParams& P = *pp;
-    extern __shared__ uint32_t shade_stack[];
+    scene_tables_to_lds(P.sc);
+    uint32_t* const shade_stack = g_scene_lds + P.sc.lds_words;  // after the scene tables
     const uint32_t s = blockIdx.x * kShadeBlock + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < kParts + 2) P.tctr[160 * parity + threadIdx.x] = 0;  // this pass's trace
     Counts cnt;
@@ -374,12 +375,12 @@ hipError_t wf_set_params(const dev::DevScene& sc, const dev::DevFrame& fr, float
 
 // One pass: shade (resolve + advance + refill + enqueue), then trace.
 hipError_t wf_launch_pass(const void* dparams, uint32_t flags, uint32_t nslots, int trace_grid, int shade_lds,
-                          int64_t pass, hipStream_t stream) {
+                          uint32_t p_lds_words, int64_t pass, hipStream_t stream) {
     const int parity = static_cast<int>(pass & 1);
     const bool full = (flags & 2u) != 0, count = (flags & 1u) != 0;
     const dev::WfParams* p = static_cast<const dev::WfParams*>(dparams);
     const dim3 gs((nslots + dev::kShadeBlock - 1) / dev::kShadeBlock), bs(dev::kShadeBlock);
-    const size_t lds = sizeof(uint32_t) * dev::kShadeBlock * static_cast<size_t>(shade_lds);
+    const size_t lds = sizeof(uint32_t) * (dev::kShadeBlock * static_cast<size_t>(shade_lds) + p_lds_words);
     if (full && count) hipLaunchKernelGGL((dev::bdpt_shade_kernel<true, true>), gs, bs, lds, stream, p, parity);
     else if (full) hipLaunchKernelGGL((dev::bdpt_shade_kernel<true, false>), gs, bs, lds, stream, p, parity);
     else if (count) hipLaunchKernelGGL((dev::bdpt_shade_kernel<false, true>), gs, bs, lds, stream, p, parity);
