@@ -33,6 +33,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import bdpt_amd  # noqa: E402
+import bdpt_dist  # noqa: E402
 import variants  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -40,11 +41,13 @@ METRIC = "Msamples/sec (whole node) at 256 spp, Cornell caustic 512², 1/2/4/8 G
 
 
 def algorithmic_bytes_per_sample(c: dict, samples: int) -> float:
-    """SURVEY.md §8(d) byte model, evaluated on this build's own counting pass:
-    64 B per interior-node visit (both child boxes + links), 48 B per triangle
-    test (3 float4 vertices), 48 B per closest hit shading record, 64 B per light
-    vertex written or read, 12 B per framebuffer add (splats + the eye estimate)."""
-    b = (64 * c["interior_visits"] + 48 * c["tri_tests"] + 48 * c["closest_rays"]
+    """SURVEY.md §8(d) byte model on this build's data layout, evaluated on its
+    own counting pass (DESIGN.md "Roofline"): 112 B per 4-wide node visit (six
+    child-bound float4 + the link float4), 48 B per triangle test (v0, e1, e2),
+    96 B per shaded closest hit (v0 + the 80-byte shading record), 64 B per
+    light vertex written or read, 12 B per framebuffer add (camera splats and
+    the per-sample eye estimate)."""
+    b = (112 * c["interior_visits"] + 48 * c["tri_tests"] + 96 * c["closest_rays"]
          + 64 * (c["light_verts"] + c["light_vert_reads"]) + 12 * (c["splats"] + samples))
     return b / max(samples, 1)
 
@@ -59,8 +62,8 @@ def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int) -> dict:
     toml = os.path.join("/tmp", f"bench_{scene}_{os.getpid()}.toml")
     with open(toml, "w") as f:
         f.write(variants.toml_text(scene, W, H, spp, rr))
-    # two rows per thread: ~12 s of wall time at the reference's ~45 us per caustic sample
-    stride = max(1, H // (2 * threads))
+    # ~6 rows per thread: 10-20 s of wall time at the reference's ~18 us per caustic sample-thread
+    stride = max(1, H // (6 * threads))
     if os.path.exists(ref):
         out = subprocess.run([ref, "render", toml, str(W), str(H), str(spp), "--rr", str(rr), "--threads",
                               str(threads), "--row-stride", str(stride)], capture_output=True, text=True,
@@ -92,6 +95,8 @@ def main() -> None:
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--rr-depth", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--schedule", choices=["megakernel", "wavefront"], default="megakernel",
+                    help="render schedule (BDPT_FLAG_WAVEFRONT for the shade/trace passes)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_caustic_512x512_256spp.json"),
                     help="measured HBM bytes per launch (rocprofv3 --pmc summary) for roofline.traffic")
     args = ap.parse_args()
@@ -116,13 +121,15 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     kernel_ms = []
+    sched_flags = bdpt_amd.FLAG_WAVEFRONT if args.schedule == "wavefront" else 0
+
+    row_offset, row_stride = bdpt_dist.row_shard(rank, world)
 
     def step():
         fb.zero_()
-        integ.render_device(fb.data_ptr(), stream, row_offset=rank, row_stride=world)
+        integ.render_device(fb.data_ptr(), stream, row_offset=row_offset, row_stride=row_stride, flags=sched_flags)
         kernel_ms.append(integ.stats()["kernel_ms"])  # waits for the render kernel's end event
-        if world > 1:
-            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+        bdpt_dist.reduce_framebuffer(fb, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -151,7 +158,7 @@ def main() -> None:
         cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=min(spp, 16), rr_depth=rr)
         cnt = bdpt_amd.BDPTIntegrator(integ.scene, cnt_cfg, device=local if world > 1 else 0)
         cbuf = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
-        cnt.render_device(cbuf.data_ptr(), stream, flags=bdpt_amd.FLAG_COUNT)
+        cnt.render_device(cbuf.data_ptr(), stream, flags=bdpt_amd.FLAG_COUNT | sched_flags)
         cst = cnt.stats()
         bps = algorithmic_bytes_per_sample(cst["counters"], cst["samples"])
         achieved = bps * local_samples / (avg_kernel_ms * 1e-3) / 1e9
@@ -179,7 +186,9 @@ def main() -> None:
                        "parallelism": f"{world}-way row-interleaved shards + RCCL sum-reduce"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
-                         "kernel": "bdpt_frame_kernel", "kernel_ms": round(avg_kernel_ms, 3),
+                         "kernel": "bdpt_frame_kernel" if args.schedule == "megakernel"
+                         else "bdpt_shade_kernel + bdpt_trace_kernel",
+                         "schedule": args.schedule, "kernel_ms": round(avg_kernel_ms, 3),
                          "bytes_per_sample": round(bps, 1),
                          "counts_per_sample": {k: round(v / cst["samples"], 3) for k, v in cst["counters"].items()}},
         }

@@ -38,10 +38,20 @@ __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame
     if (COUNT) cnt.c[any ? 1 : 0]++;
     float t, u, v;
     const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+#ifdef BDPT_PROBE_NO_TRAVERSAL  // register-pressure experiment only
+    const int res = (__float_as_int(L.ray.d.x) & 3) ? (__float_as_int(L.ray.o.y) & 1023) : -1;
+    t = L.ray.d.z * 3.f, u = L.ray.o.x * 0.1f, v = L.ray.o.z * 0.2f;
+#else
     const int res = traverse<FULL, COUNT>(sc, L.ray, any, stk, t, u, v, cnt);
+#endif
     const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t act = resolve<COUNT>(L, res, t, u, v, sc, fr, fb, cnt);
+#ifdef BDPT_PROBE_NO_ADVANCE  // register-pressure experiment only
+    L.state = act == A_FINISH ? ST_IDLE : ST_EYE;
+    L.ray.o = L.ray.o + L.ray.d;
+#else
     advance<COUNT>(L, act, sc, fr, fb, ls, cnt);
+#endif
     if (COUNT && first_active_lane()) {  // wave clocks in traversal / in the state advance
         const uint64_t c2 = __builtin_amdgcn_s_memtime();
         cnt.c[12] += static_cast<uint32_t>(c1 - c0);

@@ -207,6 +207,12 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             for (uint32_t a = A_START_LIGHT; a <= A_FINISH; a++)
                 if (__ballot(act == a) && act == a && first_active_lane()) cnt.c[11]++;
         }
+#ifdef BDPT_PROBE_SKIP  // register-pressure experiment only: drop one action's code
+        if (act == BDPT_PROBE_SKIP) {
+            act = A_FINISH;
+            continue;
+        }
+#endif
         switch (act) {
             case A_START_LIGHT: {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
                 float emitterPdf, areaPdf;
