@@ -34,7 +34,7 @@ REFERENCE_SEED = 260450963  # renderer.cpp:155
 COUNTER_NAMES = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
                  "light_vert_reads", "splats", "rng_draws", "trav_lane_iters", "trav_wave_iters",
                  "shade_lane_actions", "shade_wave_actions", "trav_clocks", "shade_clocks", "loop_clocks",
-                 "slab_fallbacks"]
+                 "slab_fallbacks", "stack_gt8", "stack_gt12", "stack_gt16", "spare"]
 
 
 class BdptError(RuntimeError):
@@ -60,7 +60,7 @@ class _SceneInfo(ctypes.Structure):
 
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
-                ("counters", ctypes.c_int64 * 16)]
+                ("counters", ctypes.c_int64 * 20)]
 
 
 def build(force: bool = False) -> str:

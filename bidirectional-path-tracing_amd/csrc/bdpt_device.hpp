@@ -17,7 +17,7 @@ constexpr float kInvPi = 0.31830988618379067154f;     // platform.h:51
 constexpr float kInvTwoPi = 0.15915494309189533577f;  // platform.h:52
 constexpr float kEpsilon = 1e-8f;                     // platform.h:56
 constexpr float kTriMinT = 0x1.0624dep-10f;           // smallest float t with (double)t > 1e-3 (accel.h:43)
-constexpr int kCounters = 16;
+constexpr int kCounters = 20;
 #ifndef BDPT_TRAV_WHILE_WHILE
 #define BDPT_TRAV_WHILE_WHILE 1  // megakernel traversal loop shape (0: one node or leaf per iteration)
 #endif
@@ -346,7 +346,10 @@ __device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_
 // lane live in LDS (entry k of thread x at lds[k * stride + x]: 8-byte lanes,
 // conflict-free), deeper ones spill to a per-lane HBM column (rare; the host
 // sizes it to the scene's worst case).
-constexpr int kLdsStack = 16;
+#ifndef BDPT_LDS_STACK
+#define BDPT_LDS_STACK 8  // traversal-stack entries per lane in LDS (deeper ones spill to HBM, rare)
+#endif
+constexpr int kLdsStack = BDPT_LDS_STACK;
 constexpr uint32_t kEmptyLinkDev = 0xffffffffu;  // unused 4-wide child slot
 struct Stack {
     uint2* lds;
@@ -559,6 +562,11 @@ __device__ __forceinline__ bool trav_node(const DevScene& sc, const Ray& r, cons
     if (lnk[3] != kEmptyLinkDev) stk.put(ts.sp++, lnk[3], key[3]);
     if (lnk[2] != kEmptyLinkDev) stk.put(ts.sp++, lnk[2], key[2]);
     if (lnk[1] != kEmptyLinkDev) stk.put(ts.sp++, lnk[1], key[1]);
+    if (COUNT) {  // stack-depth probe: entries held at depth >= 8, >= 12, >= 16
+        cnt.c[16] += ts.sp > 8 ? ts.sp - 8 : 0;
+        cnt.c[17] += ts.sp > 12 ? ts.sp - 12 : 0;
+        cnt.c[18] += ts.sp > 16 ? ts.sp - 16 : 0;
+    }
     ts.link = lnk[0];
     return true;
 }

@@ -26,7 +26,7 @@ namespace bdpt {
 namespace dev {
 
 #ifndef BDPT_WAVES_PER_EU
-#define BDPT_WAVES_PER_EU 3  // waves per SIMD the register allocator must leave room for
+#define BDPT_WAVES_PER_EU 4  // waves per SIMD the register allocator must leave room for
 #endif
 constexpr int kBlock = 256;
 
@@ -86,7 +86,8 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     const LightStore ls = light_store(kp.lv, kp.fr.rr_depth, blockIdx.x * kBlock + threadIdx.x);
     unsigned long long* const work = kp.work;
     const uint64_t total = kp.fr.total_samples;
-    Lane L;
+    __shared__ LaneCold cold_mem[kBlock];
+    Lane L(cold_mem[threadIdx.x]);
     L.state = ST_IDLE;
     bool exhausted = false;  // wave-uniform
     const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
@@ -130,19 +131,20 @@ __global__ __launch_bounds__(64) void bdpt_sample_kernel(DevScene sc, DevFrame f
     if (threadIdx.x != 0) return;
     Counts cnt;
     const LightStore ls = light_store(lvbuf, fr.rr_depth, 0);
-    Lane L;
+    __shared__ LaneCold cold_mem[1];
+    Lane L(cold_mem[0]);
     mt_seed_skip(L.rng, seed, draws);
-    L.pixel = 0;
-    L.cam_d = ray.d;
+    L.c.pixel = 0;
+    L.c.cam_d = ray.d;
     L.ray = ray;
-    L.Li = mk(0.f, 0.f, 0.f);
-    L.steps = 0;
+    L.c.Li = mk(0.f, 0.f, 0.f);
+    L.c.steps = 0;
     L.state = ST_PRIMARY;
     DevFrame f1 = fr;
     f1.flags |= kFlagNoEyeAccum;  // Integrator::render returns Li; the caller accumulates it
     const Stack stk{stack_mem, 64, kLdsStack, gstack, 1, 0};
     while (L.state != ST_IDLE) step<false, false>(L, sc, f1, fb, ls, stk, cnt);
-    out[0] = L.Li.x, out[1] = L.Li.y, out[2] = L.Li.z;
+    out[0] = L.c.Li.x, out[1] = L.c.Li.y, out[2] = L.c.Li.z;
     out[3] = __uint_as_float(L.rng.n);
 }
 

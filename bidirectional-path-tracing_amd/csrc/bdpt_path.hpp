@@ -160,36 +160,48 @@ enum : uint32_t {  // actions that need no query
     A_DONE,
 };
 
+// Per-lane state between queries. The hot part lives in registers; the part
+// only some actions touch (LaneCold) lives in LDS, one 92-byte record per
+// lane — an odd number of dwords (23), so a wave's accesses are bank-conflict free —
+// which keeps the megakernel's register allocation (and its scratch spills)
+// down without slowing the actions that use it.
+struct LaneCold {
+    f3 tp;        // subpath throughput
+    float vc, vcm;
+    f3 cam_d;     // the camera ray direction (the eye walk re-traces it, bdpt.h:59,70)
+    f3 Li;        // eye estimate of the sample
+    f3 pend;      // contribution applied if the pending shadow ray is unoccluded
+    int pend_px;  // splat pixel of a pending camera connection
+    int pixel;
+    int prim_mat;
+    int steps;    // queries issued for the current sample
+    int nl;       // stored light vertices
+    int ci;       // next light vertex to connect
+    int depth;
+    uint32_t pure;  // isPathPureSpecular
+    uint32_t pad_;  // keeps the record an odd number of dwords
+};
+static_assert(sizeof(LaneCold) == 92, "odd dword stride keeps LDS accesses conflict free");
+
 struct Lane {
     LazyMT rng;
-    int pixel;
     uint32_t state;
-    Ray ray;     // the pending query
-    f3 cam_d;    // the camera ray direction (the eye walk re-traces it, bdpt.h:59,70)
-    f3 tp;       // subpath throughput
-    float vc, vcm;
-    int depth;
-    int nl;      // stored light vertices
-    int ci;      // next light vertex to connect
-    bool pure;   // isPathPureSpecular
-    int prim_mat;
-    f3 Li;
-    Hit h;       // current subpath vertex
-    f3 pend;     // contribution applied if the pending shadow ray is unoccluded
-    int pend_px;
-    int steps;   // queries issued for the current sample
+    Ray ray;  // the pending query
+    Hit h;    // current subpath vertex
+    LaneCold& c;
+    __device__ explicit Lane(LaneCold& cold) : c(cold) {}
 };
 
 template <bool COUNT>
 __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __restrict__ fb, Counts& cnt) {
     if (COUNT) cnt.c[7] += L.rng.n;
     // rgb[p] += acc * (1 / spp) (renderer.cpp:202), one sample at a time.
-    if (!(fr.flags & kFlagNoEyeAccum) && (L.Li.x != 0.f || L.Li.y != 0.f || L.Li.z != 0.f)) {
+    if (!(fr.flags & kFlagNoEyeAccum) && (L.c.Li.x != 0.f || L.c.Li.y != 0.f || L.c.Li.z != 0.f)) {
         const float inv_spp = 1.f / static_cast<float>(fr.spp);
-        float* px = fb + 3 * static_cast<size_t>(L.pixel);
-        atomicAdd(px + 0, L.Li.x * inv_spp);
-        atomicAdd(px + 1, L.Li.y * inv_spp);
-        atomicAdd(px + 2, L.Li.z * inv_spp);
+        float* px = fb + 3 * static_cast<size_t>(L.c.pixel);
+        atomicAdd(px + 0, L.c.Li.x * inv_spp);
+        atomicAdd(px + 1, L.c.Li.y * inv_spp);
+        atomicAdd(px + 2, L.c.Li.z * inv_spp);
     }
     L.state = ST_IDLE;
 }
@@ -225,16 +237,16 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 f3 fs, ft;
                 make_frame(nOut, fs, ft);
                 L.ray = Ray{pOut, to_world(fs, ft, nOut, edir), kEpsilon, 3.402823466e+38f};
-                L.tp = (ld3(e.radiance) * edir.z) * (1.f / emissionPdf);
-                L.vc = edir.z * (1.f / emissionPdf);
-                L.vcm = areaPdf / emissionPdf;
-                L.nl = 0;
-                L.depth = 1;
+                L.c.tp = (ld3(e.radiance) * edir.z) * (1.f / emissionPdf);
+                L.c.vc = edir.z * (1.f / emissionPdf);
+                L.c.vcm = areaPdf / emissionPdf;
+                L.c.nl = 0;
+                L.c.depth = 1;
                 act = (edir.z <= 0.f) ? A_START_EYE : A_LIGHT_NEXT;
                 break;
             }
             case A_LIGHT_NEXT:  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
-                if (!(L.depth < fr.rr_depth)) {
+                if (!(L.c.depth < fr.rr_depth)) {
                     (void)next1(L.rng);
                     act = A_START_EYE;
                 } else {
@@ -245,8 +257,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             case A_LIGHT_VERTEX: {  // bdpt.h:193-209
                 const float dist2 = L.h.dist * L.h.dist;
                 const float absCosIn = fabsf(L.h.wo.z);
-                L.vcm *= (dist2 / absCosIn);
-                L.vc *= (1.f / absCosIn);
+                L.c.vcm *= (dist2 / absCosIn);
+                L.c.vc *= (1.f / absCosIn);
                 act = A_LIGHT_CONTINUE;
                 const BsdfRecord& b = bsdf_of(sc, L.h.mat);
                 if (is_delta(b)) break;
@@ -267,16 +279,16 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 const float img2surf = img2solid * (wi.z * invD2);
                 const float surf2img = 1.f / img2surf;
                 const float nlight = static_cast<float>(fr.W * fr.H);
-                f3 rad = L.tp * (f * (1.f / wi.z));
+                f3 rad = L.c.tp * (f * (1.f / wi.z));
                 rad = rad * (1.f / surf2img);
                 rad = rad * (1.f / nlight);
                 rad = rad * (1.f / static_cast<float>(fr.spp));
                 const float reversePdf_a = 1.f * img2surf;
                 const float prevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;  // swapped (wi, wo), rr = 1
-                const float lightWeight = (reversePdf_a / nlight) * (L.vcm + prevRev * L.vc);
+                const float lightWeight = (reversePdf_a / nlight) * (L.c.vcm + prevRev * L.c.vc);
                 const float mis = 1.f / (lightWeight + 1.f + 0.f);
-                L.pend = (fr.strategy == 0) ? rad * mis : rad;
-                L.pend_px = yp * fr.W + xp;
+                L.c.pend = (fr.strategy == 0) ? rad * mis : rad;
+                L.c.pend_px = yp * fr.W + xp;
                 L.ray = shadow_ray(cam_o, L.h.p);
                 L.state = ST_SPLAT;
                 act = A_ISSUED;
@@ -285,13 +297,13 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             case A_LIGHT_CONTINUE: {  // bdpt.h:211-215
                 const BsdfRecord& b = bsdf_of(sc, L.h.mat);
                 const bool delta = is_delta(b);
-                if (!delta) store_vertex(ls, L.nl, L.h, L.tp, L.vcm, L.vc, 1.f);  // the pre-walk vertex state
-                if (!continue_walk(b, L.h, L.rng, L.tp, L.depth, L.vc, L.vcm, L.ray)) {
+                if (!delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, 1.f);  // the pre-walk vertex state
+                if (!continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray)) {
                     act = A_START_EYE;
                     break;
                 }
                 if (!delta) {
-                    L.nl++;
+                    L.c.nl++;
                     if (COUNT) cnt.c[4]++;
                 }
                 act = A_LIGHT_NEXT;
@@ -299,25 +311,25 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             }
             case A_START_EYE: {  // eyeSubpathWalk prologue (bdpt.h:47-65)
                 if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
-                    L.Li = ld3(bsdf_of(sc, L.prim_mat).emission);
+                    L.c.Li = ld3(bsdf_of(sc, L.c.prim_mat).emission);
                     act = A_FINISH;
                     break;
                 }
-                const float cosCamera = dot(fwd, L.cam_d);
+                const float cosCamera = dot(fwd, L.c.cam_d);
                 const float d = fr.cam.vnear / cosCamera;
                 const float t1Pdf = 1.f * (d * d / cosCamera);
-                L.tp = mk(1.f, 1.f, 1.f);
-                L.vc = 0.f;
-                L.vcm = static_cast<float>(fr.W * fr.H) * (1.f / t1Pdf);
-                L.depth = 1;
-                L.pure = true;
-                L.Li = mk(0.f, 0.f, 0.f);
-                L.ray = Ray{cam_o, L.cam_d, 1.f, 1000.f};
+                L.c.tp = mk(1.f, 1.f, 1.f);
+                L.c.vc = 0.f;
+                L.c.vcm = static_cast<float>(fr.W * fr.H) * (1.f / t1Pdf);
+                L.c.depth = 1;
+                L.c.pure = 1u;
+                L.c.Li = mk(0.f, 0.f, 0.f);
+                L.ray = Ray{cam_o, L.c.cam_d, 1.f, 1000.f};
                 act = A_EYE_NEXT;
                 break;
             }
             case A_EYE_NEXT:  // bdpt.h:68
-                if (!(L.depth < fr.rr_depth)) {
+                if (!(L.c.depth < fr.rr_depth)) {
                     (void)next1(L.rng);
                     act = A_FINISH;
                 } else {
@@ -328,8 +340,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             case A_EYE_VERTEX: {  // bdpt.h:73-150
                 const float dist2 = L.h.dist * L.h.dist;
                 const float absCosIn = fabsf(L.h.wo.z);
-                L.vcm *= (dist2 / absCosIn);
-                L.vc *= (1.f / absCosIn);
+                L.c.vcm *= (dist2 / absCosIn);
+                L.c.vc *= (1.f / absCosIn);
                 const BsdfRecord& b = bsdf_of(sc, L.h.mat);
                 const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
                 if (!is_zero(emission)) {
@@ -337,19 +349,19 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                     if (eid >= 0) {  // (the reference asserts otherwise, integrator.cpp:56)
                         const EmitterRecord& e = emitter_of(sc, eid);
                         const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
-                        if (L.depth > 1) {
-                            f3 contrib = ld3(e.radiance) * L.tp;
+                        if (L.c.depth > 1) {
+                            f3 contrib = ld3(e.radiance) * L.c.tp;
                             const float pA = 1.f / (e.area * emitterPdf);
-                            const float camW = pA * L.vcm + (pA * kInvTwoPi) * L.vc;
+                            const float camW = pA * L.c.vcm + (pA * kInvTwoPi) * L.c.vc;
                             const float mis = 1.f / (1.f + camW);
                             if (fr.strategy == 2) {  // PATH_TRACING (bdpt.h:110-113)
-                                if (L.pure) L.Li = L.Li + contrib;
+                                if (L.c.pure) L.c.Li = L.c.Li + contrib;
                             } else {
-                                if (!L.pure) contrib = contrib * mis;
-                                L.Li = L.Li + contrib;
+                                if (!L.c.pure) contrib = contrib * mis;
+                                L.c.Li = L.c.Li + contrib;
                             }
-                        } else if (L.depth == 1) {
-                            L.Li = L.Li + emission;
+                        } else if (L.c.depth == 1) {
+                            L.c.Li = L.c.Li + emission;
                         }
                     }
                     act = A_FINISH;
@@ -359,8 +371,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                     act = A_EYE_CONTINUE;
                     break;
                 }
-                L.pure = false;
-                L.ci = 0;
+                L.c.pure = 0u;
+                L.c.ci = 0;
                 act = A_CONN;
                 // connectToLight (bdpt.h:374-430): 4 draws, then everything but visibility.
                 float emitterPdf, posPdf;
@@ -374,14 +386,14 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 const float cosAtEye = wi.z;
                 if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
                 const float pdf_w = (emitterPdf * posPdf) * d2 / cosAtLight;
-                const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * (1.f / pdf_w)) * L.tp) * ld3(e.radiance);
+                const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * (1.f / pdf_w)) * L.c.tp) * ld3(e.radiance);
                 if (is_zero(Li)) break;
                 const float lightWeight = (bsdf_pdf(b, wi, L.h.wo) * 1.f) / pdf_w;
                 const float eyePrevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;
                 const float eyeCurRev_a = cosAtEye * (1.f / d2) * kInvTwoPi;
-                const float eyeWeight = eyeCurRev_a * (L.vcm + eyePrevRev * L.vc);
+                const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
                 const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
-                L.pend = (fr.strategy == 0) ? Li * mis : Li;
+                L.c.pend = (fr.strategy == 0) ? Li * mis : Li;
                 L.ray = shadow_ray(L.h.p, ep);
                 L.state = ST_NEE;
                 act = A_ISSUED;
@@ -391,8 +403,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 act = A_EYE_CONTINUE;
                 if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
                 const BsdfRecord& be = bsdf_of(sc, L.h.mat);
-                while (L.ci < L.nl) {
-                    const Vertex V = load_vertex(ls, L.ci);
+                while (L.c.ci < L.c.nl) {
+                    const Vertex V = load_vertex(ls, L.c.ci);
                     if (COUNT) cnt.c[5]++;
                     f3 dir = L.h.p - V.p;
                     const float invD2 = 1.f / dot(dir, dir);
@@ -401,12 +413,12 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                     const f3 wiE = to_local(L.h.s, L.h.t, L.h.n, -dir);
                     const float cosL = wiL.z, cosE = wiE.z;
                     if (cosL <= 0.f || cosE <= 0.f) {
-                        L.ci++;
+                        L.c.ci++;
                         continue;
                     }
                     const BsdfRecord& bl = bsdf_of(sc, V.mat);
                     f3 Li = bsdf_eval(bl, wiL, V.wo) * bsdf_eval(be, wiE, L.h.wo);
-                    Li = Li * ((V.tp * L.tp) * invD2);
+                    Li = Li * ((V.tp * L.c.tp) * invD2);
                     const float eyePathRev_w = bsdf_pdf(bl, wiL, V.wo) * V.rr;
                     const float lightPrevRev = bsdf_pdf(bl, V.wo, wiL) * V.rr;
                     const float lightPathRev_w = bsdf_pdf(be, wiE, L.h.wo) * 1.f;
@@ -414,9 +426,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                     const float lightPathRev_a = lightPathRev_w * cosL * invD2;
                     const float eyePathRev_a = eyePathRev_w * cosE * invD2;
                     const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
-                    const float eyeWeight = eyePathRev_a * (L.vcm + eyePrevRev * L.vc);
+                    const float eyeWeight = eyePathRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
                     const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
-                    L.pend = Li * mis;
+                    L.c.pend = Li * mis;
                     L.ray = shadow_ray(L.h.p, V.p);
                     L.state = ST_CONN;
                     act = A_ISSUED;
@@ -425,7 +437,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 break;
             }
             case A_EYE_CONTINUE:  // bdpt.h:152
-                act = continue_walk(bsdf_of(sc, L.h.mat), L.h, L.rng, L.tp, L.depth, L.vc, L.vcm, L.ray) ? A_EYE_NEXT
+                act = continue_walk(bsdf_of(sc, L.h.mat), L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray) ? A_EYE_NEXT
                                                                                                        : A_FINISH;
                 break;
             case A_FINISH:
@@ -444,13 +456,13 @@ __device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame
     const uint64_t lr = s / per_row, q = s % per_row;
     const int j = static_cast<int>(q / fr.spp), k = static_cast<int>(q % fr.spp);
     const int row = fr.row_offset + static_cast<int>(lr) * fr.row_stride;
-    L.pixel = row * fr.W + j;
-    mt_seed(L.rng, fr.seed_base + static_cast<uint32_t>(L.pixel) * static_cast<uint32_t>(fr.spp) +
+    L.c.pixel = row * fr.W + j;
+    mt_seed(L.rng, fr.seed_base + static_cast<uint32_t>(L.c.pixel) * static_cast<uint32_t>(fr.spp) +
                        static_cast<uint32_t>(k));
-    L.cam_d = camera_dir(fr, L.pixel, L.rng);
-    L.ray = Ray{mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]), L.cam_d, 1.f, 1000.f};
-    L.Li = mk(0.f, 0.f, 0.f);
-    L.steps = 0;
+    L.c.cam_d = camera_dir(fr, L.c.pixel, L.rng);
+    L.ray = Ray{mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]), L.c.cam_d, 1.f, 1000.f};
+    L.c.Li = mk(0.f, 0.f, 0.f);
+    L.c.steps = 0;
     L.state = ST_PRIMARY;
 }
 
@@ -471,7 +483,7 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
         case ST_PRIMARY:
             if (!hit) act = A_FINISH;
             else {
-                L.prim_mat = L.h.mat;
+                L.c.prim_mat = L.h.mat;
                 act = (fr.strategy == 2) ? A_START_EYE : A_START_LIGHT;
             }
             break;
@@ -479,27 +491,27 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
         case ST_SPLAT:
             if (!hit) {
                 if (COUNT) cnt.c[6]++;
-                float* px = fb + 3 * static_cast<size_t>(L.pend_px);
-                atomicAdd(px + 0, L.pend.x);
-                atomicAdd(px + 1, L.pend.y);
-                atomicAdd(px + 2, L.pend.z);
+                float* px = fb + 3 * static_cast<size_t>(L.c.pend_px);
+                atomicAdd(px + 0, L.c.pend.x);
+                atomicAdd(px + 1, L.c.pend.y);
+                atomicAdd(px + 2, L.c.pend.z);
             }
             act = A_LIGHT_CONTINUE;
             break;
         case ST_EYE: act = hit ? A_EYE_VERTEX : A_FINISH; break;
         case ST_NEE:
-            if (!hit) L.Li = L.Li + L.pend;
+            if (!hit) L.c.Li = L.c.Li + L.c.pend;
             act = A_CONN;
             break;
         case ST_CONN:
-            if (!hit) L.Li = L.Li + L.pend;
-            L.ci++;
+            if (!hit) L.c.Li = L.c.Li + L.c.pend;
+            L.c.ci++;
             act = A_CONN;
             break;
         default: act = A_DONE;
     }
     // A state-machine bug must not hang the GPU: bound the queries per sample.
-    if (++L.steps > kMaxStepsPerSample && act != A_FINISH) act = A_FINISH;
+    if (++L.c.steps > kMaxStepsPerSample && act != A_FINISH) act = A_FINISH;
     return act;
 }
 

@@ -82,21 +82,21 @@ __device__ __forceinline__ void load_lane(Lane& L, const WfParams& P, uint32_t s
                  c5 = gld4(b + 5 * n), c6 = gld4(b + 6 * n), c7 = gld4(b + 7 * n), c8 = gld4(b + 8 * n),
                  c9 = gld4(b + 9 * n);
     L.rng = LazyMT{__float_as_uint(c0.x), __float_as_uint(c0.y), __float_as_uint(c0.z), __float_as_uint(c0.w)};
-    L.pixel = __float_as_int(c1.x);
+    L.c.pixel = __float_as_int(c1.x);
     const uint32_t sp = __float_as_uint(c1.y);
     L.state = sp & 0xffu;
-    L.pure = (sp >> 8) & 1u;
-    L.steps = __float_as_int(c1.z);
-    L.prim_mat = __float_as_int(c1.w);
-    L.cam_d = xyz(c2), L.vc = c2.w;
-    L.tp = xyz(c3), L.vcm = c3.w;
-    L.Li = xyz(c4), L.depth = __float_as_int(c4.w);
+    L.c.pure = (sp >> 8) & 1u;
+    L.c.steps = __float_as_int(c1.z);
+    L.c.prim_mat = __float_as_int(c1.w);
+    L.c.cam_d = xyz(c2), L.c.vc = c2.w;
+    L.c.tp = xyz(c3), L.c.vcm = c3.w;
+    L.c.Li = xyz(c4), L.c.depth = __float_as_int(c4.w);
     L.h.p = xyz(c5), L.h.dist = c5.w;
     L.h.n = xyz(c6), L.h.mat = __float_as_int(c6.w);
     L.h.wo = xyz(c7), L.h.shape = __float_as_int(c7.w);
     make_frame(L.h.n, L.h.s, L.h.t);  // Frame(n) is a pure function of n
-    L.pend = xyz(c8), L.pend_px = __float_as_int(c8.w);
-    L.nl = __float_as_int(c9.x), L.ci = __float_as_int(c9.y);
+    L.c.pend = xyz(c8), L.c.pend_px = __float_as_int(c8.w);
+    L.c.nl = __float_as_int(c9.x), L.c.ci = __float_as_int(c9.y);
     const float4 r0 = gld4(P.ray + 2 * s), r1 = gld4(P.ray + 2 * s + 1);
     L.ray = Ray{xyz(r0), xyz(r1), fabsf(r0.w), r1.w};
 }
@@ -106,15 +106,15 @@ __device__ __forceinline__ void store_lane(const Lane& L, const WfParams& P, uin
     float4* b = P.lane + s;
     gst4(b, make_float4(__uint_as_float(L.rng.a0), __uint_as_float(L.rng.a1), __uint_as_float(L.rng.b),
                         __uint_as_float(L.rng.n)));
-    gst4(b + n, f4i(L.pixel, static_cast<int>(L.state | (L.pure ? 0x100u : 0u)), L.steps, L.prim_mat));
-    gst4(b + 2 * n, f4(L.cam_d, L.vc));
-    gst4(b + 3 * n, f4(L.tp, L.vcm));
-    gst4(b + 4 * n, f4(L.Li, __int_as_float(L.depth)));
+    gst4(b + n, f4i(L.c.pixel, static_cast<int>(L.state | (L.c.pure ? 0x100u : 0u)), L.c.steps, L.c.prim_mat));
+    gst4(b + 2 * n, f4(L.c.cam_d, L.c.vc));
+    gst4(b + 3 * n, f4(L.c.tp, L.c.vcm));
+    gst4(b + 4 * n, f4(L.c.Li, __int_as_float(L.c.depth)));
     gst4(b + 5 * n, f4(L.h.p, L.h.dist));
     gst4(b + 6 * n, f4(L.h.n, __int_as_float(L.h.mat)));
     gst4(b + 7 * n, f4(L.h.wo, __int_as_float(L.h.shape)));
-    gst4(b + 8 * n, f4(L.pend, __int_as_float(L.pend_px)));
-    gst4(b + 9 * n, f4i(L.nl, L.ci, 0, 0));
+    gst4(b + 8 * n, f4(L.c.pend, __int_as_float(L.c.pend_px)));
+    gst4(b + 9 * n, f4i(L.c.nl, L.c.ci, 0, 0));
     // min_t > 0 on every query the state machine issues; its sign marks shadow rays
     gst4(P.ray + 2 * s, f4(L.ray.o, is_shadow_state(L.state) ? -L.ray.min_t : L.ray.min_t));
     gst4(P.ray + 2 * s + 1, f4(L.ray.d, L.ray.max_t));
@@ -196,9 +196,10 @@ __global__ __launch_bounds__(kShadeBlock) void bdpt_shade_kernel(const WfParams*
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     const bool valid = s < P.nslots;
-    Lane L;
+    __shared__ LaneCold cold_mem[kShadeBlock];
+    Lane L(cold_mem[threadIdx.x]);
     L.state = ST_IDLE;
-    L.pixel = 0;
+    L.c.pixel = 0;
     bool was_active = false;
     if (valid) {
         const float4 c1 = gld4(P.lane + P.nslots + s);
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(kShadeBlock) void bdpt_shade_kernel(const WfParams*
     if (valid && L.state != ST_IDLE) {
         store_lane(L, P, s);
     } else if (was_active) {  // no query: idle state, and a NaN min_t the trace pass skips
-        gst4(P.lane + P.nslots + s, f4i(L.pixel, ST_IDLE, 0, 0));
+        gst4(P.lane + P.nslots + s, f4i(L.c.pixel, ST_IDLE, 0, 0));
         gst4(P.ray + 2 * s, make_float4(0.f, 0.f, 0.f, __builtin_nanf("")));
     }
     if (COUNT) {

@@ -84,14 +84,16 @@ typedef struct {
     uint32_t flags;        /* BDPT_FLAG_* */
 } bdpt_frame_params;
 
-#define BDPT_NUM_COUNTERS 16
+#define BDPT_NUM_COUNTERS 20
 /* counters: [0] closest-hit rays, [1] shadow rays, [2] interior-node visits,
  * [3] triangle tests, [4] light vertices stored, [5] light-vertex reads,
  * [6] camera splats, [7] RNG draws; SIMD-efficiency probes: [8] traversal
  * iterations summed over lanes, [9] the same counted once per wave, [10]
  * state-machine actions summed over lanes, [11] action executions per wave;
  * wave clocks (s_memtime, summed over waves): [12] in traversal, [13] in the
- * state advance, [14] whole persistent loop; [15] exact slab fallbacks. */
+ * state advance, [14] whole persistent loop; [15] exact slab fallbacks;
+ * traversal-stack depth probes (after each 4-wide node): [16] entries held
+ * beyond depth 8, [17] beyond 12, [18] beyond 16 (the LDS part); [19] spare. */
 typedef struct {
     double kernel_ms;      /* HIP-event time of the render kernel(s) of the last call */
     int64_t samples;       /* camera samples rendered by the last call */
