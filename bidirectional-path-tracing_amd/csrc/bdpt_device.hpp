@@ -407,14 +407,14 @@ __device__ __forceinline__ bool first_active_lane() {
 // minimum t, ties to the lowest index (the reference's strict `<` in its
 // left-first DFS = leaf order). Any: true on a hit inside [min_t, max_t].
 template <bool COUNT>
-__device__ __forceinline__ bool leaf_tests(const DevScene& sc, uint32_t link, const Ray& r, bool any, float& best_t,
+__device__ __forceinline__ bool leaf_tests(const float4* __restrict__ tri, uint32_t link, const Ray& r, bool any, float& best_t,
                                            int& best, float& best_u, float& best_v, uint32_t& tri_count) {
     const uint32_t start = (link >> 3) & 0x0fffffffu, count = link & 7u;
     for (uint32_t k = 0; k < count; k++) {
         const uint32_t i = start + k;
         float t, u, v;
         if (COUNT) tri_count++;
-        if (tri_test(sc.tri, i, r, t, u, v)) {
+        if (tri_test(tri, i, r, t, u, v)) {
             if (any) {
                 if (t <= r.max_t && t >= r.min_t) {
                     best = 1;
@@ -447,7 +447,7 @@ __device__ BDPT_NOINLINE TravResult traverse_binary(const DevScene& sc, Ray r, b
     int sp = 0;
     for (;;) {
         if (link & kLeafBit) {
-            if (leaf_tests<COUNT>(sc, link, r, any, res.t, res.best, res.u, res.v, res.tris)) break;
+            if (leaf_tests<COUNT>(sc.tri, link, r, any, res.t, res.best, res.u, res.v, res.tris)) break;
         } else {
             if (COUNT) res.nodes++, res.exact += 2;
             const float4* nd = sc.nodes + 4 * static_cast<size_t>(link);
@@ -491,6 +491,26 @@ __device__ __forceinline__ int child_fast(float lx, float hx, float ly, float hy
 // test, then the cross pairs, then the reference's own divisions). Children
 // are visited near-first; stacked entries carry their entry distance and are
 // dropped on pop once a closer hit exists.
+// The scene pointers a walk needs, copied once per query into registers: the
+// DevScene lives in a parameter block in global memory, and reading a field
+// through it inside the node loop would put a dependent load in front of
+// every node fetch (the compiler must assume the block may change).
+struct TravScene {
+    const float4* __restrict__ tri;
+    const float4* __restrict__ wnodes;
+    uint32_t wroot_link;
+};
+__device__ __forceinline__ const float4* uniform_ptr(const float4* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v & 0xffffffffu)));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32)));
+    return reinterpret_cast<const float4*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+__device__ __forceinline__ TravScene trav_scene(const DevScene& sc) {
+    return TravScene{uniform_ptr(sc.tri), uniform_ptr(sc.wnodes),
+                     static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sc.wroot_link)))};
+}
+
 struct TravState {
     uint32_t link;
     int sp;
@@ -498,7 +518,7 @@ struct TravState {
     float best_t, best_u, best_v;
 };
 
-__device__ __forceinline__ TravState trav_begin(const DevScene& sc, const Ray& r) {
+__device__ __forceinline__ TravState trav_begin(const TravScene& sc, const Ray& r) {
     return TravState{sc.wroot_link, 0, -1, r.max_t, 0.f, 0.f};
 }
 
@@ -519,7 +539,7 @@ __device__ __forceinline__ bool trav_pop(const Ray& r, bool any, TravState& ts, 
 // nearest hit child (true) and stacks the others far-to-near; false when no
 // child is hit (the caller pops).
 template <bool COUNT>
-__device__ __forceinline__ bool trav_node(const DevScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
+__device__ __forceinline__ bool trav_node(const TravScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
                                           const Stack& stk, Counts& cnt) {
     if (COUNT) cnt.c[2]++;
     const float4* nd = sc.wnodes + 8 * static_cast<size_t>(ts.link);
@@ -574,14 +594,14 @@ __device__ __forceinline__ bool trav_node(const DevScene& sc, const Ray& r, cons
 // One loop iteration (a 4-wide node or a leaf, then the pop). Returns true
 // when the query is complete (result in ts.best / best_t / best_u / best_v).
 template <bool COUNT>
-__device__ __forceinline__ bool trav_step(const DevScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
+__device__ __forceinline__ bool trav_step(const TravScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
                                           const Stack& stk, Counts& cnt) {
     if (COUNT) {
         cnt.c[8]++;
         if (first_active_lane()) cnt.c[9]++;
     }
     if (ts.link & kLeafBit) {
-        if (leaf_tests<COUNT>(sc, ts.link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return true;
+        if (leaf_tests<COUNT>(sc.tri, ts.link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return true;
     } else if (trav_node<COUNT>(sc, r, ri, any, ts, stk, cnt)) {
         return false;
     }
@@ -592,7 +612,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, const Ray& r, cons
 // through interior nodes together until each holds a leaf (or is done), then
 // the leaves are tested together — a wave iteration runs one kind of work.
 template <bool COUNT>
-__device__ __forceinline__ void trav_while_while(const DevScene& sc, const Ray& r, const RayInv& ri, bool any,
+__device__ __forceinline__ void trav_while_while(const TravScene& sc, const Ray& r, const RayInv& ri, bool any,
                                                  TravState& ts, const Stack& stk, Counts& cnt) {
     for (;;) {
         bool live = true;
@@ -611,7 +631,7 @@ __device__ __forceinline__ void trav_while_while(const DevScene& sc, const Ray& 
             cnt.c[8]++;
             if (first_active_lane()) cnt.c[9]++;
         }
-        if (leaf_tests<COUNT>(sc, ts.link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return;
+        if (leaf_tests<COUNT>(sc.tri, ts.link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return;
         if (!trav_pop(r, any, ts, stk)) return;
     }
 }
@@ -627,11 +647,12 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool a
         bt = q.t, bu = q.u, bv = q.v;
         return q.best;
     }
-    TravState ts = trav_begin(sc, r);
+    const TravScene tsc = trav_scene(sc);
+    TravState ts = trav_begin(tsc, r);
 #if BDPT_TRAV_WHILE_WHILE
-    trav_while_while<COUNT>(sc, r, ri, any, ts, stk, cnt);
+    trav_while_while<COUNT>(tsc, r, ri, any, ts, stk, cnt);
 #else
-    while (!trav_step<COUNT>(sc, r, ri, any, ts, stk, cnt)) {
+    while (!trav_step<COUNT>(tsc, r, ri, any, ts, stk, cnt)) {
     }
 #endif
     bt = ts.best_t, bu = ts.best_u, bv = ts.best_v;

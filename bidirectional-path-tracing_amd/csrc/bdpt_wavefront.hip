@@ -272,6 +272,7 @@ __global__ __launch_bounds__(kTraceBlock, BDPT_TRACE_WAVES) void bdpt_trace_kern
     RayInv ri{};
     TravState ts{};
     bool exhausted = false;  // wave-uniform
+    const TravScene tsc = trav_scene(P.sc);
     int part = static_cast<int>((blockIdx.x * (kTraceBlock / 64) + wave) & (kParts - 1));
     uint64_t pending = 0;  // wave-uniform: probed slots of the chunk not dealt yet
     uint32_t cbase = 0;
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(kTraceBlock, BDPT_TRACE_WAVES) void bdpt_trace_kern
                         r = Ray{xyz(r0), xyz(r1), fabsf(r0.w), r1.w};
                         if (COUNT) cnt.c[any ? 1 : 0]++;
                         ri = ray_inv(r);  // finite and min_t <= max_t: the shade kernel took the others
-                        ts = trav_begin(P.sc, r);
+                        ts = trav_begin(tsc, r);
                         has = true;
                     }
                     __builtin_amdgcn_wave_barrier();
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(kTraceBlock, BDPT_TRACE_WAVES) void bdpt_trace_kern
             if (exhausted) break;
             continue;
         }
-        if (has && trav_step<COUNT>(P.sc, r, ri, any, ts, stk, cnt)) {
+        if (has && trav_step<COUNT>(tsc, r, ri, any, ts, stk, cnt)) {
             gst4(P.res + slot, make_float4(ts.best_t, ts.best_u, ts.best_v, __int_as_float(ts.best)));
             has = false;
         }
