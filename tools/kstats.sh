@@ -1,12 +1,13 @@
 #!/bin/bash
 # Compile-time resource report of the frame kernel<false,false>: VGPRs, scratch,
 # occupancy and code size (lines of ISA), optional extra hipcc flags as $@.
-cd "$(dirname "$0")/../bidirectional-path-tracing_amd"
+PKG="$(cd "$(dirname "$0")/../bidirectional-path-tracing_amd" && pwd)"
 T=$(mktemp -d)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Icsrc -I../include "$@" -x hip \
-  -c csrc/bdpt_kernels.hip -o $T/k.o --save-temps -Rpass-analysis=kernel-resource-usage 2> $T/rem.txt
+cd $T
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I$PKG/csrc -I$PKG/../include "$@" -x hip \
+  -c $PKG/csrc/bdpt_kernels.hip -o $T/k.o --save-temps -Rpass-analysis=kernel-resource-usage 2> $T/rem.txt < /dev/null
+S=$(ls $T/*gfx950.s 2>/dev/null) || { echo "compile failed"; grep error $T/rem.txt | head; rm -rf $T; exit 1; }
 grep -A12 'Lb0ELb0' $T/rem.txt | grep -E 'VGPRs:|SGPRs:|Scratch|Occupancy' | sed 's/.*remark: *//' | tr '\n' ' '
-S=$(ls $T/*gfx950.s 2>/dev/null || ls *gfx950.s 2>/dev/null) || { echo "compile failed"; sed -n 1,20p $T/rem.txt | grep error; exit 1; }
 awk '/^_ZN4bdpt3dev17bdpt_frame_kernelILb0ELb0EE.*:/{f=1} f{print} /s_endpgm/{if(f)exit}' $S > $T/k.s
 echo "isa_lines=$(wc -l < $T/k.s) scratch_ops=$(grep -c scratch_ $T/k.s) lanespill=$(grep -c v_writelane $T/k.s)"
-rm -rf $T bdpt_kernels-hip-* 2>/dev/null
+cd /; rm -rf $T
