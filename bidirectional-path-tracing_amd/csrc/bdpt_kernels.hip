@@ -92,8 +92,13 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     bool exhausted = false;  // wave-uniform
     const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
-        const KParams* P = kpp;
-        asm volatile("" : "+s"(P));
+        // Re-derived every iteration (opaque to the optimiser) so constants are
+        // read where they are used instead of being pinned in registers; typed
+        // as constant-address-space memory so those reads are scalar loads.
+        typedef const __attribute__((address_space(4))) KParams* ConstKParams;
+        uint64_t pa = (uint64_t)(ConstKParams)kpp;
+        asm volatile("" : "+s"(pa));
+        const KParams* P = (const KParams*)(ConstKParams)pa;
         if (!exhausted) {  // refill idle lanes: one atomic per wave
             const uint64_t idle = __ballot(L.state == ST_IDLE);
             if (idle) {
