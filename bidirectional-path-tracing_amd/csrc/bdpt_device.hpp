@@ -102,7 +102,7 @@ struct Ray {
 // Hit record = the parts of SurfaceInteraction (core.h:173-180) the path reads.
 struct Hit {
     f3 p, wo;
-    f3 s, t, n;  // frameNs
+    f3 n;  // frameNs.n; s and t are recomputed from it (Frame(n) is a pure function of n)
     float dist;
     int mat, shape;
 };
@@ -236,6 +236,18 @@ __device__ __forceinline__ void make_frame(f3 a, f3& s, f3& t) {
 __device__ __forceinline__ f3 to_local(f3 s, f3 t, f3 n, f3 v) { return mk(dot(v, s), dot(v, t), dot(v, n)); }
 __device__ __forceinline__ f3 to_world(f3 s, f3 t, f3 n, f3 v) { return (s * v.x + t * v.y) + n * v.z; }
 __device__ __forceinline__ f3 reflect_z(f3 d) { return mk(-d.x, -d.y, d.z); }
+// Shading-frame conversions at a vertex with shading normal n (the frame is
+// rebuilt on use rather than kept live in registers between queries).
+__device__ __forceinline__ f3 local_at(f3 n, f3 v) {
+    f3 s, t;
+    make_frame(n, s, t);
+    return to_local(s, t, n, v);
+}
+__device__ __forceinline__ f3 world_at(f3 n, f3 v) {
+    f3 s, t;
+    make_frame(n, s, t);
+    return to_world(s, t, n, v);
+}
 
 // ---------------------------------------------------------------- traversal
 // BBox::intersect (bvh.h:33-69): the reference's slab test, bit for bit (true
@@ -667,8 +679,9 @@ __device__ __forceinline__ void shade_hit(const DevScene& sc, int i, float u, fl
     const float w = 1 - u - v;
     h.p = (v0 * w + v1 * u) + v2 * v;
     h.n = normalize((xyz(s0) * w + xyz(s1) * u) + xyz(s2) * v);
-    make_frame(h.n, h.s, h.t);
-    h.wo = to_local(h.s, h.t, h.n, -dir);
+    f3 fs, ft;
+    make_frame(h.n, fs, ft);
+    h.wo = to_local(fs, ft, h.n, -dir);
     h.dist = t;
     h.mat = __float_as_int(s0.w);
     h.shape = __float_as_int(s1.w);

@@ -83,7 +83,7 @@ __device__ __forceinline__ bool continue_walk(const BsdfRecord& b, const Hit& h,
         vc = (absCosOut / pdf) * (vcm + prevRev * vc);
         vcm = 1.f / pdf;
     }
-    ray = Ray{h.p, to_world(h.s, h.t, h.n, wi), kEpsilon, 3.402823466e+38f};  // FLT_MAX (core.h:120)
+    ray = Ray{h.p, world_at(h.n, wi), kEpsilon, 3.402823466e+38f};  // FLT_MAX (core.h:120)
     return true;
 }
 
@@ -271,7 +271,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 if (xp < 0 || yp < 0 || xp >= fr.W || yp >= fr.H) break;
                 const float cosCamera = dot(fwd, e2l);
                 if (cosCamera <= 0.f) break;
-                const f3 wi = to_local(L.h.s, L.h.t, L.h.n, -e2l);
+                const f3 wi = local_at(L.h.n, -e2l);
                 const f3 f = bsdf_eval(b, wi, L.h.wo);
                 if (is_zero(f) || wi.z <= 0.f) break;
                 const float d = fr.cam.vnear / cosCamera;
@@ -381,7 +381,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 f3 dir = L.h.p - ep;
                 const float d2 = dot(dir, dir);
                 dir = dir * (1.f / sqrt_cr(d2));
-                const f3 wi = to_local(L.h.s, L.h.t, L.h.n, -dir);
+                const f3 wi = local_at(L.h.n, -dir);
                 const float cosAtLight = dot(en, dir);
                 const float cosAtEye = wi.z;
                 if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
@@ -410,7 +410,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                     const float invD2 = 1.f / dot(dir, dir);
                     dir = dir * sqrt_cr(invD2);
                     const f3 wiL = to_local(V.s, V.t, V.n, dir);
-                    const f3 wiE = to_local(L.h.s, L.h.t, L.h.n, -dir);
+                    const f3 wiE = local_at(L.h.n, -dir);
                     const float cosL = wiL.z, cosE = wiE.z;
                     if (cosL <= 0.f || cosE <= 0.f) {
                         L.c.ci++;

@@ -94,7 +94,6 @@ __device__ __forceinline__ void load_lane(Lane& L, const WfParams& P, uint32_t s
     L.h.p = xyz(c5), L.h.dist = c5.w;
     L.h.n = xyz(c6), L.h.mat = __float_as_int(c6.w);
     L.h.wo = xyz(c7), L.h.shape = __float_as_int(c7.w);
-    make_frame(L.h.n, L.h.s, L.h.t);  // Frame(n) is a pure function of n
     L.c.pend = xyz(c8), L.c.pend_px = __float_as_int(c8.w);
     L.c.nl = __float_as_int(c9.x), L.c.ci = __float_as_int(c9.y);
     const float4 r0 = gld4(P.ray + 2 * s), r1 = gld4(P.ray + 2 * s + 1);
