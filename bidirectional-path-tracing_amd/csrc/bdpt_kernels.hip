@@ -29,6 +29,12 @@ namespace dev {
 #define BDPT_WAVES_PER_EU 4  // waves per SIMD the register allocator must leave room for
 #endif
 constexpr int kBlock = 256;
+#ifndef BDPT_OVERLAP
+#define BDPT_OVERLAP 1  // overlapped walk / shade schedule in the megakernel (0: one query then shade, in lockstep)
+#endif
+#ifndef BDPT_SHADE_READY
+#define BDPT_SHADE_READY 56  // lanes with a finished query that trigger the wave's shading step
+#endif
 
 // One query for the lane's pending state, then the state advance.
 template <bool FULL, bool COUNT>
@@ -90,6 +96,14 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     Lane L(cold_mem[threadIdx.x]);
     L.state = ST_IDLE;
     bool exhausted = false;  // wave-uniform
+#if BDPT_OVERLAP
+    const TravScene tsc = trav_scene(kp.sc);
+    bool tracing = false, has_res = false, q_any = false;
+    TravState ts{};
+    RayInv ri{};
+    int res = -1;
+    float rt = 0.f, ru = 0.f, rv = 0.f;
+#endif
     const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
         // Re-derived every iteration (opaque to the optimiser) so constants are
@@ -118,7 +132,54 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             if (exhausted) break;
             continue;
         }
+#if BDPT_OVERLAP
+        // Overlapped schedule: lanes keep walking their query across loop
+        // iterations; a lane whose query finished waits (result kept) until
+        // enough lanes of the wave are ready, then those lanes shade together
+        // while the slow walkers resume afterwards from where they stopped.
+        if (L.state != ST_IDLE && !tracing && !has_res) {  // a new query: begin its walk
+            q_any = is_shadow_state(L.state);
+            if (COUNT) cnt.c[q_any ? 1 : 0]++;
+            ri = ray_inv(L.ray);
+            if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root (bvh.h:277, :287)
+                res = -1, rt = L.ray.max_t, ru = rv = 0.f;
+                has_res = true;
+            } else if (FULL || !ri.fast) {
+                const TravResult q = traverse_binary<COUNT, Stack>(P->sc, L.ray, q_any, !FULL, stk);
+                if (COUNT) cnt.c[2] += q.nodes, cnt.c[3] += q.tris, cnt.c[15] += q.exact;
+                res = q.best, rt = q.t, ru = q.u, rv = q.v;
+                has_res = true;
+            } else {
+                ts = trav_begin(tsc, L.ray);
+                tracing = true;
+            }
+        }
+        const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+        for (;;) {  // walk until enough lanes have a result to shade
+            const uint64_t tr = __ballot(tracing);
+            if (!tr) break;
+            const uint64_t ready = __ballot(has_res);
+            if (__popcll(ready) >= BDPT_SHADE_READY) break;
+            if (tracing && trav_step<COUNT>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
+                res = ts.best, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;
+                tracing = false;
+                has_res = true;
+            }
+        }
+        const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+        if (has_res) {
+            has_res = false;
+            const uint32_t act = resolve<COUNT>(L, res, rt, ru, rv, P->sc, P->fr, P->fb, cnt);
+            advance<COUNT>(L, act, P->sc, P->fr, P->fb, ls, cnt);
+        }
+        if (COUNT && first_active_lane()) {
+            const uint64_t c2 = __builtin_amdgcn_s_memtime();
+            cnt.c[12] += static_cast<uint32_t>(c1 - c0);
+            cnt.c[13] += static_cast<uint32_t>(c2 - c1);
+        }
+#else
         if (L.state != ST_IDLE) step<FULL, COUNT>(L, P->sc, P->fr, P->fb, ls, stk, cnt);
+#endif
     }
     if (COUNT) {
         if (lane == 0) cnt.c[14] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - clock0);
