@@ -40,18 +40,36 @@ struct Vertex {  // PathVertex (bdpt.h:24-35)
     int mat;
 };
 
+#ifndef BDPT_LV_NT
+#define BDPT_LV_NT 0  // 1: light-vertex records use non-temporal loads / stores (keep L2 for the scene)
+#endif
+__device__ __forceinline__ void lv_st(float4* p, float4 x) {
+#if BDPT_LV_NT
+    __builtin_nontemporal_store(v4f_t{x.x, x.y, x.z, x.w}, (__attribute__((address_space(1))) v4f_t*)(p));
+#else
+    gst4(p, x);
+#endif
+}
+__device__ __forceinline__ float4 lv_ld(const float4* p) {
+#if BDPT_LV_NT
+    const v4f_t v = __builtin_nontemporal_load((const __attribute__((address_space(1))) v4f_t*)(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return gld4(p);
+#endif
+}
 __device__ __forceinline__ void store_vertex(const LightStore& ls, int v, const Hit& h, f3 tp, float vcm, float vc,
                                              float rr) {
     float4* q = ls.at(v);
-    gst4(q, make_float4(h.p.x, h.p.y, h.p.z, vcm));
-    gst4(q + 1, make_float4(h.n.x, h.n.y, h.n.z, vc));
-    gst4(q + 2, make_float4(h.wo.x, h.wo.y, h.wo.z, rr));
-    gst4(q + 3, make_float4(tp.x, tp.y, tp.z, __int_as_float(h.mat)));
+    lv_st(q, make_float4(h.p.x, h.p.y, h.p.z, vcm));
+    lv_st(q + 1, make_float4(h.n.x, h.n.y, h.n.z, vc));
+    lv_st(q + 2, make_float4(h.wo.x, h.wo.y, h.wo.z, rr));
+    lv_st(q + 3, make_float4(tp.x, tp.y, tp.z, __int_as_float(h.mat)));
 }
 
 __device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
     const float4* q = ls.at(v);
-    const float4 a = gld4(q), b = gld4(q + 1), c = gld4(q + 2), d = gld4(q + 3);
+    const float4 a = lv_ld(q), b = lv_ld(q + 1), c = lv_ld(q + 2), d = lv_ld(q + 3);
     Vertex x;
     x.p = xyz(a), x.vcm = a.w;
     x.n = xyz(b), x.vc = b.w;
