@@ -336,10 +336,10 @@ __device__ __forceinline__ bool box_test(float lx, float ly, float lz, float hx,
     return slab(lx, ly, lz, hx, hy, hz, r, tn, tf);
 }
 
-// rayTriangleIntersect (core.h:379-400) + accel.h:43's t > 1e-3.
-__device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_t i, const Ray& r, float& t, float& u,
-                                         float& v) {
-    const f3 v0 = xyz(gld4(tri + 3 * i)), e1 = xyz(gld4(tri + 3 * i + 1)), e2 = xyz(gld4(tri + 3 * i + 2));
+// rayTriangleIntersect (core.h:379-400) + accel.h:43's t > 1e-3, on the
+// triangle's v0 and edges (e1 = v1 - v0, e2 = v2 - v0 rounded as the
+// reference rounds them).
+__device__ __forceinline__ bool tri_test_edges(f3 v0, f3 e1, f3 e2, const Ray& r, float& t, float& u, float& v) {
     const f3 pvec = cross(r.d, e2);
     const float det = dot(e1, pvec);
     if (fabsf(det) < kEpsilon) return false;
@@ -352,6 +352,10 @@ __device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_
     if (v < 0.f || u + v > 1.f) return false;
     t = dot(e2, qvec) * invDet;
     return t >= kTriMinT;
+}
+__device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_t i, const Ray& r, float& t, float& u,
+                                         float& v) {
+    return tri_test_edges(xyz(gld4(tri + 3 * i)), xyz(gld4(tri + 3 * i + 1)), xyz(gld4(tri + 3 * i + 2)), r, t, u, v);
 }
 
 // Traversal stack of (link, t_near) entries: the first kLdsStack entries of a
@@ -418,15 +422,32 @@ __device__ __forceinline__ bool first_active_lane() {
 // Triangle tests of one reference leaf (bvh.h:291-309). Closest: keeps the
 // minimum t, ties to the lowest index (the reference's strict `<` in its
 // left-first DFS = leaf order). Any: true on a hit inside [min_t, max_t].
+// The triangles are fetched BDPT_LEAF_GROUP at a time with all their loads in
+// flight together (one memory round trip per group instead of two per
+// triangle); indices past the leaf's count are clamped and their results unused.
+#ifndef BDPT_LEAF_GROUP
+#define BDPT_LEAF_GROUP 1
+#endif
+#ifndef BDPT_LEAF_PIPELINE
+#define BDPT_LEAF_PIPELINE 0  // 1: fetch triangle k + 1 while testing triangle k
+#endif
 template <bool COUNT>
 __device__ __forceinline__ bool leaf_tests(const float4* __restrict__ tri, uint32_t link, const Ray& r, bool any, float& best_t,
                                            int& best, float& best_u, float& best_v, uint32_t& tri_count) {
+    constexpr uint32_t G = BDPT_LEAF_GROUP;
     const uint32_t start = (link >> 3) & 0x0fffffffu, count = link & 7u;
+#if BDPT_LEAF_PIPELINE
+    float4 n0 = gld4(tri + 3 * start), n1 = gld4(tri + 3 * start + 1), n2 = gld4(tri + 3 * start + 2);
     for (uint32_t k = 0; k < count; k++) {
+        const float4 a0 = n0, a1 = n1, a2 = n2;
+        const uint32_t nx = start + (k + 1 < count ? k + 1 : k);
+        n0 = gld4(tri + 3 * nx), n1 = gld4(tri + 3 * nx + 1), n2 = gld4(tri + 3 * nx + 2);
+        asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a2.x), "v"(a2.y),
+                     "v"(a2.z));
         const uint32_t i = start + k;
         float t, u, v;
         if (COUNT) tri_count++;
-        if (tri_test(tri, i, r, t, u, v)) {
+        if (tri_test_edges(xyz(a0), xyz(a1), xyz(a2), r, t, u, v)) {
             if (any) {
                 if (t <= r.max_t && t >= r.min_t) {
                     best = 1;
@@ -434,6 +455,38 @@ __device__ __forceinline__ bool leaf_tests(const float4* __restrict__ tri, uint3
                 }
             } else if (t < best_t || (t == best_t && best >= 0 && static_cast<int>(i) < best)) {
                 best_t = t, best = static_cast<int>(i), best_u = u, best_v = v;
+            }
+        }
+    }
+    return false;
+#endif
+    for (uint32_t k0 = 0; k0 < count; k0 += G) {
+        float4 q[G][3];
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) {
+            const uint32_t i = start + (k0 + g < count ? k0 + g : count - 1);
+            q[g][0] = gld4(tri + 3 * i), q[g][1] = gld4(tri + 3 * i + 1), q[g][2] = gld4(tri + 3 * i + 2);
+        }
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) asm volatile("" ::"v"(q[g][j].x), "v"(q[g][j].y), "v"(q[g][j].z));
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) {
+            const uint32_t k = k0 + g;
+            if (k >= count) break;
+            const uint32_t i = start + k;
+            float t, u, v;
+            if (COUNT) tri_count++;
+            if (tri_test_edges(xyz(q[g][0]), xyz(q[g][1]), xyz(q[g][2]), r, t, u, v)) {
+                if (any) {
+                    if (t <= r.max_t && t >= r.min_t) {
+                        best = 1;
+                        return true;
+                    }
+                } else if (t < best_t || (t == best_t && best >= 0 && static_cast<int>(i) < best)) {
+                    best_t = t, best = static_cast<int>(i), best_u = u, best_v = v;
+                }
             }
         }
     }
