@@ -34,7 +34,7 @@ REFERENCE_SEED = 260450963  # renderer.cpp:155
 COUNTER_NAMES = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
                  "light_vert_reads", "splats", "rng_draws", "trav_lane_iters", "trav_wave_iters",
                  "shade_lane_actions", "shade_wave_actions", "trav_clocks", "shade_clocks", "loop_clocks",
-                 "slab_fallbacks", "stack_gt8", "stack_gt12", "stack_gt16", "spare"]
+                 "slab_fallbacks", "stack_gt8", "stack_gt12", "stack_gt16", "pop_culled"]
 
 
 class BdptError(RuntimeError):

@@ -589,13 +589,15 @@ __device__ __forceinline__ TravState trav_begin(const TravScene& sc, const Ray& 
 
 // Pops the nearest pending entry that can still hold a closer hit; false when
 // the traversal is complete.
-__device__ __forceinline__ bool trav_pop(const Ray& r, bool any, TravState& ts, const Stack& stk) {
+__device__ __forceinline__ bool trav_pop(const Ray& r, bool any, TravState& ts, const Stack& stk,
+                                         uint32_t* culled = nullptr) {
     while (ts.sp > 0) {
         const uint2 e = stk.get(--ts.sp);
         if (!(__uint_as_float(e.y) > cull_far(any ? r.max_t : ts.best_t))) {
             ts.link = e.x;
             return true;
         }
+        if (culled) (*culled)++;
     }
     return false;
 }
@@ -670,7 +672,7 @@ __device__ __forceinline__ bool trav_step(const TravScene& sc, const Ray& r, con
     } else if (trav_node<COUNT>(sc, r, ri, any, ts, stk, cnt)) {
         return false;
     }
-    return !trav_pop(r, any, ts, stk);
+    return !trav_pop(r, any, ts, stk, COUNT ? &cnt.c[19] : nullptr);
 }
 
 // The same walk as a while-while loop (Aila & Laine 2009): lanes descend

@@ -93,7 +93,7 @@ typedef struct {
  * wave clocks (s_memtime, summed over waves): [12] in traversal, [13] in the
  * state advance, [14] whole persistent loop; [15] exact slab fallbacks;
  * traversal-stack depth probes (after each 4-wide node): [16] entries held
- * beyond depth 8, [17] beyond 12, [18] beyond 16 (the LDS part); [19] spare. */
+ * beyond depth 8, [17] beyond 12, [18] beyond 16; [19] stack entries culled on pop. */
 typedef struct {
     double kernel_ms;      /* HIP-event time of the render kernel(s) of the last call */
     int64_t samples;       /* camera samples rendered by the last call */
