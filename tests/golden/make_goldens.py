@@ -39,9 +39,12 @@ FRAMEBUFFERS = {
     # bench resolution: every 16th row of 512x512 at 4 spp (splats land everywhere)
     "G6_caustic_512x512_spp4_rows16": ("caustic", 512, 512, 4, 8, 16),
     "G7_hardlight_512x512_spp4_rows32": ("hardlight", 512, 512, 4, 2, 32),
+    # synthetic 1M-triangle box (scenes/synth.py), BASELINE configs[4] at a small size
+    "G8_synth1m_48x32_spp2": ("synth1m", 48, 32, 2, 8, 1),
 }
 
-SCENE_DUMPS = {"cbox_low": (64, 64), "caustic": (512, 512), "hardlight": (512, 512), "hardlight_mirror": (512, 512)}
+SCENE_DUMPS = {"cbox_low": (64, 64), "caustic": (512, 512), "hardlight": (512, 512), "hardlight_mirror": (512, 512),
+               "synth1m": (64, 64)}
 
 
 def sha(b: bytes) -> str:
@@ -49,18 +52,27 @@ def sha(b: bytes) -> str:
 
 
 def main() -> None:
+    """python make_goldens.py [NAME ...]: regenerate everything, or only the named
+    framebuffer / scene entries (merged into the existing manifest)."""
+    only = set(sys.argv[1:])
     if not os.path.exists(REF):
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle", "ref")], check=True)
+    old = {}
+    if only and os.path.exists(os.path.join(HERE, "manifest.json")):
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            old = json.load(f)
     manifest = {
         "generator": "oracle/_ref/ref_bdpt (reference sources @ /root/reference, oracle/ref/Makefile)",
         "compiler": subprocess.run(["g++", "--version"], capture_output=True, text=True).stdout.splitlines()[0],
         "glibc": platform.libc_ver()[1],
         "seed_convention": "Sampler((int)(260450963u + pixel*spp + k)); jitter next2D first when spp > 1",
-        "framebuffers": {},
-        "scenes": {},
+        "framebuffers": dict(old.get("framebuffers", {})),
+        "scenes": dict(old.get("scenes", {})),
     }
     tmp = tempfile.mkdtemp()
     for name, (scene, W, H, spp, rr, stride) in FRAMEBUFFERS.items():
+        if only and name not in only:
+            continue
         toml = os.path.join(tmp, name + ".toml")
         with open(toml, "w") as f:
             f.write(variants.toml_text(scene, W, H, spp, rr))
@@ -78,6 +90,8 @@ def main() -> None:
                                               ref_seconds=info["seconds"])
         print(name, manifest["framebuffers"][name]["sha256"][:16], info)
     for scene, (W, H) in SCENE_DUMPS.items():
+        if only and scene not in only:
+            continue
         toml = os.path.join(tmp, scene + "_dump.toml")
         with open(toml, "w") as f:
             f.write(variants.toml_text(scene, W, H, 1))

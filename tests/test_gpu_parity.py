@@ -21,7 +21,7 @@ TOL = 1e-4
 
 FB_CASES = ["G1_cbox_low_64x64_spp4", "G2_caustic_64x64_spp16", "G3_hardlight_64x64_spp16",
             "G4_hardlight_mirror_64x64_spp16", "G5_caustic_80x48_spp1", "G6_caustic_512x512_spp4_rows16",
-            "G7_hardlight_512x512_spp4_rows32"]
+            "G7_hardlight_512x512_spp4_rows32", "G8_synth1m_48x32_spp2"]
 
 _scenes = {}
 

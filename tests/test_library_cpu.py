@@ -45,7 +45,7 @@ def test_no_device_is_an_error_not_a_fallback():
         bdpt_amd.BDPTIntegrator(scene, bdpt_amd.Config())
 
 
-@pytest.mark.parametrize("scene_name", ["cbox_low", "caustic", "hardlight", "hardlight_mirror"])
+@pytest.mark.parametrize("scene_name", ["cbox_low", "caustic", "hardlight", "hardlight_mirror", "synth1m"])
 def test_ingest_matches_reference(scene_name, golden_manifest):
     meta = golden_manifest["scenes"][scene_name]
     s = bdpt_amd.Scene(variants.obj_path(scene_name))

@@ -16,7 +16,7 @@ from conftest import load_golden
 
 FB_CASES = ["G1_cbox_low_64x64_spp4", "G2_caustic_64x64_spp16", "G3_hardlight_64x64_spp16",
             "G4_hardlight_mirror_64x64_spp16", "G5_caustic_80x48_spp1", "G6_caustic_512x512_spp4_rows16",
-            "G7_hardlight_512x512_spp4_rows32"]
+            "G7_hardlight_512x512_spp4_rows32", "G8_synth1m_48x32_spp2"]
 
 
 @pytest.mark.parametrize("name", FB_CASES)
@@ -34,7 +34,7 @@ def test_oracle_framebuffer_bit_exact(name, golden_manifest):
     assert mism.size == 0, f"{mism.size} floats differ, first at {mism[:5]}"
 
 
-@pytest.mark.parametrize("scene_name", ["cbox_low", "caustic", "hardlight", "hardlight_mirror"])
+@pytest.mark.parametrize("scene_name", ["cbox_low", "caustic", "hardlight", "hardlight_mirror", "synth1m"])
 def test_oracle_scene_ingest_matches_reference(scene_name, golden_manifest):
     meta = golden_manifest["scenes"][scene_name]
     scene = O.Scene(variants.obj_path(scene_name))
