@@ -3,7 +3,7 @@
  * A plain-C restatement of the reference's algorithm
  * (JackMinn/Bidirectional-Path-Tracing: src/integrators/bdpt.h and the BSDFs,
  * BVH traversal, sampler, warps and scene ingest it calls). Each function in
- * oracle/src/*.c cites the reference file:line it restates.
+ * each oracle/src C file cites the reference file:line it restates.
  *
  * Who may use it: tests/ (as the checker), __graft_entry__.smoke() and
  * bench.py's cpu_baseline leg. The product library under
