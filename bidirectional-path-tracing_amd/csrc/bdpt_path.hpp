@@ -187,11 +187,11 @@ struct LaneCold {
     f3 tp;        // subpath throughput
     float vc, vcm;
     f3 cam_d;     // the camera ray direction (the eye walk re-traces it, bdpt.h:59,70)
-    f3 Li;        // eye estimate of the sample
+    f3 Li;        // eye estimate of the sample; during the light walk: the primary hit's (t, u, v)
     f3 pend;      // contribution applied if the pending shadow ray is unoccluded
     int pend_px;  // splat pixel of a pending camera connection
     int pixel;
-    int prim_mat;
+    int prim_tri;  // primary hit triangle (its t, u, v sit in Li until the eye walk starts)
     int steps;    // queries issued for the current sample
     int nl;       // stored light vertices
     int ci;       // next light vertex to connect
@@ -328,8 +328,10 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 break;
             }
             case A_START_EYE: {  // eyeSubpathWalk prologue (bdpt.h:47-65)
+                const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
                 if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
-                    L.c.Li = ld3(bsdf_of(sc, L.c.prim_mat).emission);
+                    const int mat = __float_as_int(gld4(sc.shade + 5 * static_cast<size_t>(L.c.prim_tri)).w);
+                    L.c.Li = ld3(bsdf_of(sc, mat).emission);
                     act = A_FINISH;
                     break;
                 }
@@ -344,6 +346,14 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 L.c.Li = mk(0.f, 0.f, 0.f);
                 L.ray = Ray{cam_o, L.c.cam_d, 1.f, 1000.f};
                 act = A_EYE_NEXT;
+                if (1 < fr.rr_depth) {
+                    // The eye walk's first intersect (bdpt.h:70) re-traces render()'s
+                    // primary ray (bdpt.h:225): same ray, same scene, so the same
+                    // (accepted) hit. It is reused instead of traced again.
+                    shade_hit(sc, L.c.prim_tri, prim.y, prim.z, prim.x, L.ray.d, L.h);
+                    L.c.steps++;
+                    act = A_EYE_VERTEX;
+                }
                 break;
             }
             case A_EYE_NEXT:  // bdpt.h:68
@@ -501,7 +511,8 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
         case ST_PRIMARY:
             if (!hit) act = A_FINISH;
             else {
-                L.c.prim_mat = L.h.mat;
+                L.c.prim_tri = res;
+                L.c.Li = mk(t, u, v);
                 act = (fr.strategy == 2) ? A_START_EYE : A_START_LIGHT;
             }
             break;

@@ -25,7 +25,7 @@
 // the reference's); only the order of framebuffer additions differs.
 //
 // Slot state, HBM (float4 chunks, chunk k of slot s at lane[k * nslots + s]):
-//   c0 rng a0 a1 b n   c1 pixel, state | pure << 8, steps, prim_mat
+//   c0 rng a0 a1 b n   c1 pixel, state | pure << 8, steps, prim_tri
 //   c2 cam_d, vc       c3 tp, vcm        c4 Li, depth      c5 hit p, dist
 //   c6 hit n, mat      c7 hit wo, shape  c8 pend, pend_px  c9 nl, ci
 // ray[2 s] = (o, min_t), ray[2 s + 1] = (d, max_t); res[s] = (t, u, v, leaf-
@@ -87,7 +87,7 @@ __device__ __forceinline__ void load_lane(Lane& L, const WfParams& P, uint32_t s
     L.state = sp & 0xffu;
     L.c.pure = (sp >> 8) & 1u;
     L.c.steps = __float_as_int(c1.z);
-    L.c.prim_mat = __float_as_int(c1.w);
+    L.c.prim_tri = __float_as_int(c1.w);
     L.c.cam_d = xyz(c2), L.c.vc = c2.w;
     L.c.tp = xyz(c3), L.c.vcm = c3.w;
     L.c.Li = xyz(c4), L.c.depth = __float_as_int(c4.w);
@@ -105,7 +105,7 @@ __device__ __forceinline__ void store_lane(const Lane& L, const WfParams& P, uin
     float4* b = P.lane + s;
     gst4(b, make_float4(__uint_as_float(L.rng.a0), __uint_as_float(L.rng.a1), __uint_as_float(L.rng.b),
                         __uint_as_float(L.rng.n)));
-    gst4(b + n, f4i(L.c.pixel, static_cast<int>(L.state | (L.c.pure ? 0x100u : 0u)), L.c.steps, L.c.prim_mat));
+    gst4(b + n, f4i(L.c.pixel, static_cast<int>(L.state | (L.c.pure ? 0x100u : 0u)), L.c.steps, L.c.prim_tri));
     gst4(b + 2 * n, f4(L.c.cam_d, L.c.vc));
     gst4(b + 3 * n, f4(L.c.tp, L.c.vcm));
     gst4(b + 4 * n, f4(L.c.Li, __int_as_float(L.c.depth)));
