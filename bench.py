@@ -37,6 +37,13 @@ import bdpt_dist  # noqa: E402
 import variants  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SCENE_LABEL = {
+    "caustic": "CausticSample (cbox_mirror.obj)",
+    "hardlight": "HardLightSample (bonus_bdpt cbox.obj)",
+    "hardlight_mirror": "HardLightSample, sphere as perfect mirror (illum 3)",
+    "cbox_low": "diffuse Cornell box (cbox_low.obj)",
+    "synth1m": "synthetic 1M-triangle box (scenes/synth.py)",
+}
 METRIC = "Msamples/sec (whole node) at 256 spp, Cornell caustic 512², 1/2/4/8 GPUs"
 
 
@@ -180,8 +187,9 @@ def main() -> None:
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic camera samples over the reference's own CausticSample scene files",
-            "config": {"workload": f"{args.scene}_{W}x{H}_{spp}spp", "scene": "CausticSample (cbox_mirror.obj)",
+            "data": ("synthetic camera samples over the reference's own scene files" if args.scene != "synth1m"
+                     else "synthetic camera samples over a generated 1M-triangle scene"),
+            "config": {"workload": f"{args.scene}_{W}x{H}_{spp}spp", "scene": SCENE_LABEL.get(args.scene, args.scene),
                        "width": W, "height": H, "spp": spp, "rr_depth": rr, "samples_per_step": samples_total,
                        "parallelism": f"{world}-way row-interleaved shards + RCCL sum-reduce"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

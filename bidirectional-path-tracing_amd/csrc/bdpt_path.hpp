@@ -224,259 +224,251 @@ __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __res
     L.state = ST_IDLE;
 }
 
-// Advances a lane from action `act` until it issues its next query or ends its sample.
-template <bool COUNT>
-__device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
-                        const LightStore& ls, Counts& cnt) {
-    const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
-    const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
-    while (act != A_ISSUED && act != A_DONE) {
-        if (COUNT) {
-            cnt.c[10]++;
-            // one wave-level execution per distinct action present among active lanes
-            for (uint32_t a = A_START_LIGHT; a <= A_FINISH; a++)
-                if (__ballot(act == a) && act == a && first_active_lane()) cnt.c[11]++;
-        }
-#ifdef BDPT_PROBE_SKIP  // register-pressure experiment only: drop one action's code
-        if (act == BDPT_PROBE_SKIP) {
-            act = A_FINISH;
-            continue;
-        }
-#endif
-        switch (act) {
-            case A_START_LIGHT: {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
-                float emitterPdf, areaPdf;
-                f3 nOut, pOut;
-                const EmitterRecord& e = sample_emitter(sc, L.rng, emitterPdf, nOut, pOut, areaPdf);
-                const f3 edir = uniform_hemisphere(next2(L.rng));
-                float emissionPdf = kInvTwoPi * areaPdf;
-                areaPdf *= emitterPdf;
-                emissionPdf *= emitterPdf;
-                f3 fs, ft;
-                make_frame(nOut, fs, ft);
-                L.ray = Ray{pOut, to_world(fs, ft, nOut, edir), kEpsilon, 3.402823466e+38f};
-                L.c.tp = (ld3(e.radiance) * edir.z) * (1.f / emissionPdf);
-                L.c.vc = edir.z * (1.f / emissionPdf);
-                L.c.vcm = areaPdf / emissionPdf;
-                L.c.nl = 0;
-                L.c.depth = 1;
-                act = (edir.z <= 0.f) ? A_START_EYE : A_LIGHT_NEXT;
-                break;
-            }
-            case A_LIGHT_NEXT:  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
-                if (!(L.c.depth < fr.rr_depth)) {
-                    (void)next1(L.rng);
-                    act = A_START_EYE;
-                } else {
-                    L.state = ST_LIGHT;
-                    act = A_ISSUED;
-                }
-                break;
-            case A_LIGHT_VERTEX: {  // bdpt.h:193-209
-                const float dist2 = L.h.dist * L.h.dist;
-                const float absCosIn = fabsf(L.h.wo.z);
-                L.c.vcm *= (dist2 / absCosIn);
-                L.c.vc *= (1.f / absCosIn);
-                act = A_LIGHT_CONTINUE;
-                const BsdfRecord& b = bsdf_of(sc, L.h.mat);
-                if (is_delta(b)) break;
-                // connectToCamera (bdpt.h:295-371): everything but the visibility test.
-                f3 e2l = L.h.p - cam_o;
-                const float invD2 = 1.f / dot(e2l, e2l);
-                e2l = e2l * sqrt_cr(invD2);
-                int xp, yp;
-                splat_pixel(fr.cam, L.h.p, xp, yp);
-                if (xp < 0 || yp < 0 || xp >= fr.W || yp >= fr.H) break;
-                const float cosCamera = dot(fwd, e2l);
-                if (cosCamera <= 0.f) break;
-                const f3 wi = local_at(L.h.n, -e2l);
-                const f3 f = bsdf_eval(b, wi, L.h.wo);
-                if (is_zero(f) || wi.z <= 0.f) break;
-                const float d = fr.cam.vnear / cosCamera;
-                const float img2solid = d * d / cosCamera;
-                const float img2surf = img2solid * (wi.z * invD2);
-                const float surf2img = 1.f / img2surf;
-                const float nlight = static_cast<float>(fr.W * fr.H);
-                f3 rad = L.c.tp * (f * (1.f / wi.z));
-                rad = rad * (1.f / surf2img);
-                rad = rad * (1.f / nlight);
-                rad = rad * (1.f / static_cast<float>(fr.spp));
-                const float reversePdf_a = 1.f * img2surf;
-                const float prevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;  // swapped (wi, wo), rr = 1
-                const float lightWeight = (reversePdf_a / nlight) * (L.c.vcm + prevRev * L.c.vc);
-                const float mis = 1.f / (lightWeight + 1.f + 0.f);
-                L.c.pend = (fr.strategy == 0) ? rad * mis : rad;
-                L.c.pend_px = yp * fr.W + xp;
-                L.ray = shadow_ray(cam_o, L.h.p);
-                L.state = ST_SPLAT;
-                act = A_ISSUED;
-                break;
-            }
-            case A_LIGHT_CONTINUE: {  // bdpt.h:211-215
-                const BsdfRecord& b = bsdf_of(sc, L.h.mat);
-                const bool delta = is_delta(b);
-                if (!delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, 1.f);  // the pre-walk vertex state
-                if (!continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray)) {
-                    act = A_START_EYE;
-                    break;
-                }
-                if (!delta) {
-                    L.c.nl++;
-                    if (COUNT) cnt.c[4]++;
-                }
-                act = A_LIGHT_NEXT;
-                break;
-            }
-            case A_START_EYE: {  // eyeSubpathWalk prologue (bdpt.h:47-65)
-                const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
-                if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
-                    const int mat = __float_as_int(gld4(sc.shade + 5 * static_cast<size_t>(L.c.prim_tri)).w);
-                    L.c.Li = ld3(bsdf_of(sc, mat).emission);
-                    act = A_FINISH;
-                    break;
-                }
-                const float cosCamera = dot(fwd, L.c.cam_d);
-                const float d = fr.cam.vnear / cosCamera;
-                const float t1Pdf = 1.f * (d * d / cosCamera);
-                L.c.tp = mk(1.f, 1.f, 1.f);
-                L.c.vc = 0.f;
-                L.c.vcm = static_cast<float>(fr.W * fr.H) * (1.f / t1Pdf);
-                L.c.depth = 1;
-                L.c.pure = 1u;
-                L.c.Li = mk(0.f, 0.f, 0.f);
-                L.ray = Ray{cam_o, L.c.cam_d, 1.f, 1000.f};
-                act = A_EYE_NEXT;
-                if (1 < fr.rr_depth) {
-                    // The eye walk's first intersect (bdpt.h:70) re-traces render()'s
-                    // primary ray (bdpt.h:225): same ray, same scene, so the same
-                    // (accepted) hit. It is reused instead of traced again.
-                    shade_hit(sc, L.c.prim_tri, prim.y, prim.z, prim.x, L.ray.d, L.h);
-                    L.c.steps++;
-                    act = A_EYE_VERTEX;
-                }
-                break;
-            }
-            case A_EYE_NEXT:  // bdpt.h:68
-                if (!(L.c.depth < fr.rr_depth)) {
-                    (void)next1(L.rng);
-                    act = A_FINISH;
-                } else {
-                    L.state = ST_EYE;
-                    act = A_ISSUED;
-                }
-                break;
-            case A_EYE_VERTEX: {  // bdpt.h:73-150
-                const float dist2 = L.h.dist * L.h.dist;
-                const float absCosIn = fabsf(L.h.wo.z);
-                L.c.vcm *= (dist2 / absCosIn);
-                L.c.vc *= (1.f / absCosIn);
-                const BsdfRecord& b = bsdf_of(sc, L.h.mat);
-                const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
-                if (!is_zero(emission)) {
-                    const int eid = shape_emitter_of(sc, L.h.shape);
-                    if (eid >= 0) {  // (the reference asserts otherwise, integrator.cpp:56)
-                        const EmitterRecord& e = emitter_of(sc, eid);
-                        const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
-                        if (L.c.depth > 1) {
-                            f3 contrib = ld3(e.radiance) * L.c.tp;
-                            const float pA = 1.f / (e.area * emitterPdf);
-                            const float camW = pA * L.c.vcm + (pA * kInvTwoPi) * L.c.vc;
-                            const float mis = 1.f / (1.f + camW);
-                            if (fr.strategy == 2) {  // PATH_TRACING (bdpt.h:110-113)
-                                if (L.c.pure) L.c.Li = L.c.Li + contrib;
-                            } else {
-                                if (!L.c.pure) contrib = contrib * mis;
-                                L.c.Li = L.c.Li + contrib;
-                            }
-                        } else if (L.c.depth == 1) {
-                            L.c.Li = L.c.Li + emission;
-                        }
-                    }
-                    act = A_FINISH;
-                    break;
-                }
-                if (is_delta(b)) {
-                    act = A_EYE_CONTINUE;
-                    break;
-                }
-                L.c.pure = 0u;
-                L.c.ci = 0;
-                act = A_CONN;
-                // connectToLight (bdpt.h:374-430): 4 draws, then everything but visibility.
-                float emitterPdf, posPdf;
-                f3 en, ep;
-                const EmitterRecord& e = sample_emitter(sc, L.rng, emitterPdf, en, ep, posPdf);
-                f3 dir = L.h.p - ep;
-                const float d2 = dot(dir, dir);
-                dir = dir * (1.f / sqrt_cr(d2));
-                const f3 wi = local_at(L.h.n, -dir);
-                const float cosAtLight = dot(en, dir);
-                const float cosAtEye = wi.z;
-                if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
-                const float pdf_w = (emitterPdf * posPdf) * d2 / cosAtLight;
-                const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * (1.f / pdf_w)) * L.c.tp) * ld3(e.radiance);
-                if (is_zero(Li)) break;
-                const float lightWeight = (bsdf_pdf(b, wi, L.h.wo) * 1.f) / pdf_w;
-                const float eyePrevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;
-                const float eyeCurRev_a = cosAtEye * (1.f / d2) * kInvTwoPi;
-                const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
-                const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
-                L.c.pend = (fr.strategy == 0) ? Li * mis : Li;
-                L.ray = shadow_ray(L.h.p, ep);
-                L.state = ST_NEE;
-                act = A_ISSUED;
-                break;
-            }
-            case A_CONN: {  // connectVertices (bdpt.h:434-483) with light vertex ci
-                act = A_EYE_CONTINUE;
-                if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
-                const BsdfRecord& be = bsdf_of(sc, L.h.mat);
-                while (L.c.ci < L.c.nl) {
-                    const Vertex V = load_vertex(ls, L.c.ci);
-                    if (COUNT) cnt.c[5]++;
-                    f3 dir = L.h.p - V.p;
-                    const float invD2 = 1.f / dot(dir, dir);
-                    dir = dir * sqrt_cr(invD2);
-                    const f3 wiL = to_local(V.s, V.t, V.n, dir);
-                    const f3 wiE = local_at(L.h.n, -dir);
-                    const float cosL = wiL.z, cosE = wiE.z;
-                    if (cosL <= 0.f || cosE <= 0.f) {
-                        L.c.ci++;
-                        continue;
-                    }
-                    const BsdfRecord& bl = bsdf_of(sc, V.mat);
-                    f3 Li = bsdf_eval(bl, wiL, V.wo) * bsdf_eval(be, wiE, L.h.wo);
-                    Li = Li * ((V.tp * L.c.tp) * invD2);
-                    const float eyePathRev_w = bsdf_pdf(bl, wiL, V.wo) * V.rr;
-                    const float lightPrevRev = bsdf_pdf(bl, V.wo, wiL) * V.rr;
-                    const float lightPathRev_w = bsdf_pdf(be, wiE, L.h.wo) * 1.f;
-                    const float eyePrevRev = bsdf_pdf(be, L.h.wo, wiE) * 1.f;
-                    const float lightPathRev_a = lightPathRev_w * cosL * invD2;
-                    const float eyePathRev_a = eyePathRev_w * cosE * invD2;
-                    const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
-                    const float eyeWeight = eyePathRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
-                    const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
-                    L.c.pend = Li * mis;
-                    L.ray = shadow_ray(L.h.p, V.p);
-                    L.state = ST_CONN;
-                    act = A_ISSUED;
-                    break;
-                }
-                break;
-            }
-            case A_EYE_CONTINUE:  // bdpt.h:152
-                act = continue_walk(bsdf_of(sc, L.h.mat), L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray) ? A_EYE_NEXT
-                                                                                                       : A_FINISH;
-                break;
-            case A_FINISH:
-                finish<COUNT>(L, fr, fb, cnt);
-                act = A_DONE;
-                break;
-            default:
-                act = A_DONE;
-        }
+// Advances a lane from action `act` until it issues its next query or ends its
+// sample. The actions form a DAG between queries (no action leads back to an
+// earlier one without a query), so one forward sweep in topological order runs
+// every lane's whole chain: each action body executes at most once per call,
+// for all lanes that reach it, wherever they entered the chain. (A loop over a
+// switch would re-run a body for every lane that reached it one step later.)
+#define BDPT_ACTION(X)                        \
+    if (COUNT) tally_action(cnt, act == (X)); \
+    if (act == (X)) do
+__device__ __forceinline__ void tally_action(Counts& cnt, bool on) {
+    if (on) {
+        cnt.c[10]++;
+        if (first_active_lane()) cnt.c[11]++;  // one wave-level execution of this body
     }
 }
+
+template <bool COUNT>
+__device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
+                    const LightStore& ls, Counts& cnt) {
+    const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
+    const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
+    BDPT_ACTION(A_START_LIGHT) {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
+        float emitterPdf, areaPdf;
+        f3 nOut, pOut;
+        const EmitterRecord& e = sample_emitter(sc, L.rng, emitterPdf, nOut, pOut, areaPdf);
+        const f3 edir = uniform_hemisphere(next2(L.rng));
+        float emissionPdf = kInvTwoPi * areaPdf;
+        areaPdf *= emitterPdf;
+        emissionPdf *= emitterPdf;
+        f3 fs, ft;
+        make_frame(nOut, fs, ft);
+        L.ray = Ray{pOut, to_world(fs, ft, nOut, edir), kEpsilon, 3.402823466e+38f};
+        L.c.tp = (ld3(e.radiance) * edir.z) * (1.f / emissionPdf);
+        L.c.vc = edir.z * (1.f / emissionPdf);
+        L.c.vcm = areaPdf / emissionPdf;
+        L.c.nl = 0;
+        L.c.depth = 1;
+        act = (edir.z <= 0.f) ? A_START_EYE : A_LIGHT_NEXT;
+    } while (0);
+    BDPT_ACTION(A_LIGHT_VERTEX) {  // bdpt.h:193-209
+        const float dist2 = L.h.dist * L.h.dist;
+        const float absCosIn = fabsf(L.h.wo.z);
+        L.c.vcm *= (dist2 / absCosIn);
+        L.c.vc *= (1.f / absCosIn);
+        act = A_LIGHT_CONTINUE;
+        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
+        if (is_delta(b)) break;
+        // connectToCamera (bdpt.h:295-371): everything but the visibility test.
+        f3 e2l = L.h.p - cam_o;
+        const float invD2 = 1.f / dot(e2l, e2l);
+        e2l = e2l * sqrt_cr(invD2);
+        int xp, yp;
+        splat_pixel(fr.cam, L.h.p, xp, yp);
+        if (xp < 0 || yp < 0 || xp >= fr.W || yp >= fr.H) break;
+        const float cosCamera = dot(fwd, e2l);
+        if (cosCamera <= 0.f) break;
+        const f3 wi = local_at(L.h.n, -e2l);
+        const f3 f = bsdf_eval(b, wi, L.h.wo);
+        if (is_zero(f) || wi.z <= 0.f) break;
+        const float d = fr.cam.vnear / cosCamera;
+        const float img2solid = d * d / cosCamera;
+        const float img2surf = img2solid * (wi.z * invD2);
+        const float surf2img = 1.f / img2surf;
+        const float nlight = static_cast<float>(fr.W * fr.H);
+        f3 rad = L.c.tp * (f * (1.f / wi.z));
+        rad = rad * (1.f / surf2img);
+        rad = rad * (1.f / nlight);
+        rad = rad * (1.f / static_cast<float>(fr.spp));
+        const float reversePdf_a = 1.f * img2surf;
+        const float prevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;  // swapped (wi, wo), rr = 1
+        const float lightWeight = (reversePdf_a / nlight) * (L.c.vcm + prevRev * L.c.vc);
+        const float mis = 1.f / (lightWeight + 1.f + 0.f);
+        L.c.pend = (fr.strategy == 0) ? rad * mis : rad;
+        L.c.pend_px = yp * fr.W + xp;
+        L.ray = shadow_ray(cam_o, L.h.p);
+        L.state = ST_SPLAT;
+        act = A_ISSUED;
+    } while (0);
+    BDPT_ACTION(A_LIGHT_CONTINUE) {  // bdpt.h:211-215
+        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
+        const bool delta = is_delta(b);
+        if (!delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, 1.f);  // the pre-walk vertex state
+        if (!continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray)) {
+            act = A_START_EYE;
+            break;
+        }
+        if (!delta) {
+            L.c.nl++;
+            if (COUNT) cnt.c[4]++;
+        }
+        act = A_LIGHT_NEXT;
+    } while (0);
+    BDPT_ACTION(A_LIGHT_NEXT) {  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
+        if (!(L.c.depth < fr.rr_depth)) {
+            (void)next1(L.rng);
+            act = A_START_EYE;
+        } else {
+            L.state = ST_LIGHT;
+            act = A_ISSUED;
+        }
+    } while (0);
+    BDPT_ACTION(A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
+        const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
+        if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
+            const int mat = __float_as_int(gld4(sc.shade + 5 * static_cast<size_t>(L.c.prim_tri)).w);
+            L.c.Li = ld3(bsdf_of(sc, mat).emission);
+            act = A_FINISH;
+            break;
+        }
+        const float cosCamera = dot(fwd, L.c.cam_d);
+        const float d = fr.cam.vnear / cosCamera;
+        const float t1Pdf = 1.f * (d * d / cosCamera);
+        L.c.tp = mk(1.f, 1.f, 1.f);
+        L.c.vc = 0.f;
+        L.c.vcm = static_cast<float>(fr.W * fr.H) * (1.f / t1Pdf);
+        L.c.depth = 1;
+        L.c.pure = 1u;
+        L.c.Li = mk(0.f, 0.f, 0.f);
+        L.ray = Ray{cam_o, L.c.cam_d, 1.f, 1000.f};
+        act = A_EYE_NEXT;
+        if (1 < fr.rr_depth) {
+            // The eye walk's first intersect (bdpt.h:70) re-traces render()'s
+            // primary ray (bdpt.h:225): same ray, same scene, so the same
+            // (accepted) hit. It is reused instead of traced again.
+            shade_hit(sc, L.c.prim_tri, prim.y, prim.z, prim.x, L.ray.d, L.h);
+            L.c.steps++;
+            act = A_EYE_VERTEX;
+        }
+    } while (0);
+    BDPT_ACTION(A_EYE_VERTEX) {  // bdpt.h:73-150
+        const float dist2 = L.h.dist * L.h.dist;
+        const float absCosIn = fabsf(L.h.wo.z);
+        L.c.vcm *= (dist2 / absCosIn);
+        L.c.vc *= (1.f / absCosIn);
+        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
+        const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
+        if (!is_zero(emission)) {
+            const int eid = shape_emitter_of(sc, L.h.shape);
+            if (eid >= 0) {  // (the reference asserts otherwise, integrator.cpp:56)
+                const EmitterRecord& e = emitter_of(sc, eid);
+                const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
+                if (L.c.depth > 1) {
+                    f3 contrib = ld3(e.radiance) * L.c.tp;
+                    const float pA = 1.f / (e.area * emitterPdf);
+                    const float camW = pA * L.c.vcm + (pA * kInvTwoPi) * L.c.vc;
+                    const float mis = 1.f / (1.f + camW);
+                    if (fr.strategy == 2) {  // PATH_TRACING (bdpt.h:110-113)
+                        if (L.c.pure) L.c.Li = L.c.Li + contrib;
+                    } else {
+                        if (!L.c.pure) contrib = contrib * mis;
+                        L.c.Li = L.c.Li + contrib;
+                    }
+                } else if (L.c.depth == 1) {
+                    L.c.Li = L.c.Li + emission;
+                }
+            }
+            act = A_FINISH;
+            break;
+        }
+        if (is_delta(b)) {
+            act = A_EYE_CONTINUE;
+            break;
+        }
+        L.c.pure = 0u;
+        L.c.ci = 0;
+        act = A_CONN;
+        // connectToLight (bdpt.h:374-430): 4 draws, then everything but visibility.
+        float emitterPdf, posPdf;
+        f3 en, ep;
+        const EmitterRecord& e = sample_emitter(sc, L.rng, emitterPdf, en, ep, posPdf);
+        f3 dir = L.h.p - ep;
+        const float d2 = dot(dir, dir);
+        dir = dir * (1.f / sqrt_cr(d2));
+        const f3 wi = local_at(L.h.n, -dir);
+        const float cosAtLight = dot(en, dir);
+        const float cosAtEye = wi.z;
+        if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
+        const float pdf_w = (emitterPdf * posPdf) * d2 / cosAtLight;
+        const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * (1.f / pdf_w)) * L.c.tp) * ld3(e.radiance);
+        if (is_zero(Li)) break;
+        const float lightWeight = (bsdf_pdf(b, wi, L.h.wo) * 1.f) / pdf_w;
+        const float eyePrevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;
+        const float eyeCurRev_a = cosAtEye * (1.f / d2) * kInvTwoPi;
+        const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
+        const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
+        L.c.pend = (fr.strategy == 0) ? Li * mis : Li;
+        L.ray = shadow_ray(L.h.p, ep);
+        L.state = ST_NEE;
+        act = A_ISSUED;
+    } while (0);
+    BDPT_ACTION(A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
+        act = A_EYE_CONTINUE;
+        if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
+        const BsdfRecord& be = bsdf_of(sc, L.h.mat);
+        while (L.c.ci < L.c.nl) {
+            const Vertex V = load_vertex(ls, L.c.ci);
+            if (COUNT) cnt.c[5]++;
+            f3 dir = L.h.p - V.p;
+            const float invD2 = 1.f / dot(dir, dir);
+            dir = dir * sqrt_cr(invD2);
+            const f3 wiL = to_local(V.s, V.t, V.n, dir);
+            const f3 wiE = local_at(L.h.n, -dir);
+            const float cosL = wiL.z, cosE = wiE.z;
+            if (cosL <= 0.f || cosE <= 0.f) {
+                L.c.ci++;
+                continue;
+            }
+            const BsdfRecord& bl = bsdf_of(sc, V.mat);
+            f3 Li = bsdf_eval(bl, wiL, V.wo) * bsdf_eval(be, wiE, L.h.wo);
+            Li = Li * ((V.tp * L.c.tp) * invD2);
+            const float eyePathRev_w = bsdf_pdf(bl, wiL, V.wo) * V.rr;
+            const float lightPrevRev = bsdf_pdf(bl, V.wo, wiL) * V.rr;
+            const float lightPathRev_w = bsdf_pdf(be, wiE, L.h.wo) * 1.f;
+            const float eyePrevRev = bsdf_pdf(be, L.h.wo, wiE) * 1.f;
+            const float lightPathRev_a = lightPathRev_w * cosL * invD2;
+            const float eyePathRev_a = eyePathRev_w * cosE * invD2;
+            const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
+            const float eyeWeight = eyePathRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
+            const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
+            L.c.pend = Li * mis;
+            L.ray = shadow_ray(L.h.p, V.p);
+            L.state = ST_CONN;
+            act = A_ISSUED;
+            break;
+        }
+    } while (0);
+    BDPT_ACTION(A_EYE_CONTINUE) {  // bdpt.h:152
+        const bool more = continue_walk(bsdf_of(sc, L.h.mat), L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray);
+        act = more ? A_EYE_NEXT : A_FINISH;
+    } while (0);
+    BDPT_ACTION(A_EYE_NEXT) {  // bdpt.h:68
+        if (!(L.c.depth < fr.rr_depth)) {
+            (void)next1(L.rng);
+            act = A_FINISH;
+        } else {
+            L.state = ST_EYE;
+            act = A_ISSUED;
+        }
+    } while (0);
+    BDPT_ACTION(A_FINISH) {
+        finish<COUNT>(L, fr, fb, cnt);
+        act = A_DONE;
+    } while (0);
+}
+#undef BDPT_ACTION
 
 // Starts sample `s` of the shard on this lane: seed, camera ray, primary query.
 __device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame& fr) {
