@@ -903,8 +903,9 @@ __device__ __forceinline__ int cdf_sample(const float* cdf, int ncdf, float u) {
 }
 
 // selectEmitter + sampleEmitterPosition (integrator.cpp:46-51, :73-100): 4 draws.
-__device__ __forceinline__ const EmitterRecord& sample_emitter(const DevScene& sc, LazyMT& rng, float& emitter_pdf,
-                                                              f3& n, f3& pos, float& pos_pdf) {
+// Returns the emitter index.
+__device__ __forceinline__ int sample_emitter(const DevScene& sc, LazyMT& rng, float& emitter_pdf, f3& n, f3& pos,
+                                              float& pos_pdf) {
     const float u0 = next1(rng);
     uint32_t id = static_cast<uint32_t>(u0 * static_cast<float>(sc.nemit));
     id = id < static_cast<uint32_t>(sc.nemit - 1) ? id : static_cast<uint32_t>(sc.nemit - 1);
@@ -920,7 +921,7 @@ __device__ __forceinline__ const EmitterRecord& sample_emitter(const DevScene& s
     pos = (v0 * w + v1 * uv.x) + v2 * uv.y;
     n = normalize((n0 * w + n1 * uv.x) + n2 * uv.y);
     pos_pdf = 1.f / e.area;
-    return e;
+    return static_cast<int>(id);
 }
 
 }  // namespace dev

@@ -40,24 +40,14 @@ constexpr int kBlock = 256;
 template <bool FULL, bool COUNT>
 __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
                                      const LightStore& ls, const Stack& stk, Counts& cnt) {
-    const bool any = is_shadow_state(L.state);
-    if (COUNT) cnt.c[any ? 1 : 0]++;
-    float t, u, v;
+    const bool any = is_shadow_state(L.state), query = L.state != ST_DEFER;
+    if (COUNT && query) cnt.c[any ? 1 : 0]++;
+    float t = 0.f, u = 0.f, v = 0.f;
     const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
-#ifdef BDPT_PROBE_NO_TRAVERSAL  // register-pressure experiment only
-    const int res = (__float_as_int(L.ray.d.x) & 3) ? (__float_as_int(L.ray.o.y) & 1023) : -1;
-    t = L.ray.d.z * 3.f, u = L.ray.o.x * 0.1f, v = L.ray.o.z * 0.2f;
-#else
-    const int res = traverse<FULL, COUNT>(sc, L.ray, any, stk, t, u, v, cnt);
-#endif
+    const int res = query ? traverse<FULL, COUNT>(sc, L.ray, any, stk, t, u, v, cnt) : -1;
     const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t act = resolve<COUNT>(L, res, t, u, v, sc, fr, fb, cnt);
-#ifdef BDPT_PROBE_NO_ADVANCE  // register-pressure experiment only
-    L.state = act == A_FINISH ? ST_IDLE : ST_EYE;
-    L.ray.o = L.ray.o + L.ray.d;
-#else
     advance<COUNT>(L, act, sc, fr, fb, ls, cnt);
-#endif
     if (COUNT && first_active_lane()) {  // wave clocks in traversal / in the state advance
         const uint64_t c2 = __builtin_amdgcn_s_memtime();
         cnt.c[12] += static_cast<uint32_t>(c1 - c0);
@@ -139,9 +129,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // while the slow walkers resume afterwards from where they stopped.
         if (L.state != ST_IDLE && !tracing && !has_res) {  // a new query: begin its walk
             q_any = is_shadow_state(L.state);
-            if (COUNT) cnt.c[q_any ? 1 : 0]++;
+            if (COUNT && L.state != ST_DEFER) cnt.c[q_any ? 1 : 0]++;
             ri = ray_inv(L.ray);
-            if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root (bvh.h:277, :287)
+            if (L.state == ST_DEFER) {  // no query: the deferred action runs in this shading step
+                res = -1;
+                has_res = true;
+            } else if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root (bvh.h:277, :287)
                 res = -1, rt = L.ray.max_t, ru = rv = 0.f;
                 has_res = true;
             } else if (FULL || !ri.fast) {

@@ -162,10 +162,12 @@ enum : uint32_t {  // the query a lane waits on
     ST_EYE,      // eyeSubpathWalk closest hit (bdpt.h:70)
     ST_NEE,      // connectToLight visibility (bdpt.h:405)
     ST_CONN,     // connectVertices visibility (bdpt.h:451)
+    ST_DEFER,    // no query: the lane resumes at A_START_EYE in the next shading step
 };
 enum : uint32_t {  // actions that need no query
     A_ISSUED = 0,
     A_START_LIGHT,
+    A_NEE,  // connectToLight after the emitter sample
     A_LIGHT_NEXT,
     A_LIGHT_VERTEX,
     A_LIGHT_CONTINUE,
@@ -225,14 +227,18 @@ __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __res
 }
 
 // Advances a lane from action `act` until it issues its next query or ends its
-// sample. The actions form a DAG between queries (no action leads back to an
-// earlier one without a query), so one forward sweep in topological order runs
-// every lane's whole chain: each action body executes at most once per call,
-// for all lanes that reach it, wherever they entered the chain. (A loop over a
-// switch would re-run a body for every lane that reached it one step later.)
-#define BDPT_ACTION(X)                        \
-    if (COUNT) tally_action(cnt, act == (X)); \
-    if (act == (X)) do
+// sample. The actions form a DAG between queries, so one forward sweep in
+// topological order runs every lane's whole chain: each action body executes at
+// most once per call, for all lanes that reach it wherever they entered the
+// chain (a loop over a switch would re-run a body for every lane that reached it
+// one step later). Work two actions share runs in one body: the emitter sample
+// of lightSubpathWalk and connectToLight, and ContinuePathRandomWalk of both
+// subpaths. The only edges against this order — a light subpath that ends at its
+// BSDF sample or its depth cap and starts the eye subpath — are deferred to the
+// next shading step (ST_DEFER) instead of being run by a second sweep.
+#define BDPT_ACTION(COND)                     \
+    if (COUNT) tally_action(cnt, (COND));     \
+    if (COND) do
 __device__ __forceinline__ void tally_action(Counts& cnt, bool on) {
     if (on) {
         cnt.c[10]++;
@@ -242,28 +248,130 @@ __device__ __forceinline__ void tally_action(Counts& cnt, bool on) {
 
 template <bool COUNT>
 __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
-                    const LightStore& ls, Counts& cnt) {
+                        const LightStore& ls, Counts& cnt) {
     const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
     const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
-    BDPT_ACTION(A_START_LIGHT) {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
-        float emitterPdf, areaPdf;
-        f3 nOut, pOut;
-        const EmitterRecord& e = sample_emitter(sc, L.rng, emitterPdf, nOut, pOut, areaPdf);
+    BDPT_ACTION(act == A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
+        const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
+        if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
+            const int mat = __float_as_int(gld4(sc.shade + 5 * static_cast<size_t>(L.c.prim_tri)).w);
+            L.c.Li = ld3(bsdf_of(sc, mat).emission);
+            act = A_FINISH;
+            break;
+        }
+        const float cosCamera = dot(fwd, L.c.cam_d);
+        const float d = fr.cam.vnear / cosCamera;
+        const float t1Pdf = 1.f * (d * d / cosCamera);
+        L.c.tp = mk(1.f, 1.f, 1.f);
+        L.c.vc = 0.f;
+        L.c.vcm = static_cast<float>(fr.W * fr.H) * (1.f / t1Pdf);
+        L.c.depth = 1;
+        L.c.pure = 1u;
+        L.c.Li = mk(0.f, 0.f, 0.f);
+        L.ray = Ray{cam_o, L.c.cam_d, 1.f, 1000.f};
+        act = A_EYE_NEXT;
+        if (1 < fr.rr_depth) {
+            // The eye walk's first intersect (bdpt.h:70) re-traces render()'s
+            // primary ray (bdpt.h:225): same ray, same scene, so the same
+            // (accepted) hit. It is reused instead of traced again.
+            shade_hit(sc, L.c.prim_tri, prim.y, prim.z, prim.x, L.ray.d, L.h);
+            L.c.steps++;
+            act = A_EYE_VERTEX;
+        }
+    } while (0);
+    BDPT_ACTION(act == A_EYE_VERTEX) {  // bdpt.h:73-136
+        const float dist2 = L.h.dist * L.h.dist;
+        const float absCosIn = fabsf(L.h.wo.z);
+        L.c.vcm *= (dist2 / absCosIn);
+        L.c.vc *= (1.f / absCosIn);
+        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
+        const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
+        if (!is_zero(emission)) {
+            const int eid = shape_emitter_of(sc, L.h.shape);
+            if (eid >= 0) {  // (the reference asserts otherwise, integrator.cpp:56)
+                const EmitterRecord& e = emitter_of(sc, eid);
+                const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
+                if (L.c.depth > 1) {
+                    f3 contrib = ld3(e.radiance) * L.c.tp;
+                    const float pA = 1.f / (e.area * emitterPdf);
+                    const float camW = pA * L.c.vcm + (pA * kInvTwoPi) * L.c.vc;
+                    const float mis = 1.f / (1.f + camW);
+                    if (fr.strategy == 2) {  // PATH_TRACING (bdpt.h:110-113)
+                        if (L.c.pure) L.c.Li = L.c.Li + contrib;
+                    } else {
+                        if (!L.c.pure) contrib = contrib * mis;
+                        L.c.Li = L.c.Li + contrib;
+                    }
+                } else if (L.c.depth == 1) {
+                    L.c.Li = L.c.Li + emission;
+                }
+            }
+            act = A_FINISH;
+            break;
+        }
+        if (is_delta(b)) {
+            act = A_EYE_CONTINUE;
+            break;
+        }
+        L.c.pure = 0u;
+        L.c.ci = 0;
+        act = A_NEE;
+    } while (0);
+    // The emitter sample (4 draws) of lightSubpathWalk (bdpt.h:162-163) and of
+    // connectToLight (bdpt.h:376-381): selectEmitter + sampleEmitterPosition.
+    int e_id = 0;
+    float e_pdf = 0.f, e_pos_pdf = 0.f;
+    f3 e_n = mk(0.f, 0.f, 0.f), e_p = e_n;
+    BDPT_ACTION(act == A_START_LIGHT || act == A_NEE) {
+        e_id = sample_emitter(sc, L.rng, e_pdf, e_n, e_p, e_pos_pdf);
+    } while (0);
+    BDPT_ACTION(act == A_START_LIGHT) {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
+        const EmitterRecord& e = emitter_of(sc, e_id);
+        float areaPdf = e_pos_pdf;
         const f3 edir = uniform_hemisphere(next2(L.rng));
         float emissionPdf = kInvTwoPi * areaPdf;
-        areaPdf *= emitterPdf;
-        emissionPdf *= emitterPdf;
+        areaPdf *= e_pdf;
+        emissionPdf *= e_pdf;
         f3 fs, ft;
-        make_frame(nOut, fs, ft);
-        L.ray = Ray{pOut, to_world(fs, ft, nOut, edir), kEpsilon, 3.402823466e+38f};
+        make_frame(e_n, fs, ft);
+        L.ray = Ray{e_p, to_world(fs, ft, e_n, edir), kEpsilon, 3.402823466e+38f};
         L.c.tp = (ld3(e.radiance) * edir.z) * (1.f / emissionPdf);
         L.c.vc = edir.z * (1.f / emissionPdf);
         L.c.vcm = areaPdf / emissionPdf;
         L.c.nl = 0;
         L.c.depth = 1;
-        act = (edir.z <= 0.f) ? A_START_EYE : A_LIGHT_NEXT;
+        if (edir.z <= 0.f) {  // bdpt.h:179-182 (the eye subpath follows)
+            L.state = ST_DEFER;
+            act = A_ISSUED;
+        } else {
+            act = A_LIGHT_NEXT;
+        }
     } while (0);
-    BDPT_ACTION(A_LIGHT_VERTEX) {  // bdpt.h:193-209
+    BDPT_ACTION(act == A_NEE) {  // connectToLight (bdpt.h:374-430): everything but the visibility test
+        act = A_CONN;
+        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
+        const EmitterRecord& e = emitter_of(sc, e_id);
+        f3 dir = L.h.p - e_p;
+        const float d2 = dot(dir, dir);
+        dir = dir * (1.f / sqrt_cr(d2));
+        const f3 wi = local_at(L.h.n, -dir);
+        const float cosAtLight = dot(e_n, dir);
+        const float cosAtEye = wi.z;
+        if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
+        const float pdf_w = (e_pdf * e_pos_pdf) * d2 / cosAtLight;
+        const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * (1.f / pdf_w)) * L.c.tp) * ld3(e.radiance);
+        if (is_zero(Li)) break;
+        const float lightWeight = (bsdf_pdf(b, wi, L.h.wo) * 1.f) / pdf_w;
+        const float eyePrevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;
+        const float eyeCurRev_a = cosAtEye * (1.f / d2) * kInvTwoPi;
+        const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
+        const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
+        L.c.pend = (fr.strategy == 0) ? Li * mis : Li;
+        L.ray = shadow_ray(L.h.p, e_p);
+        L.state = ST_NEE;
+        act = A_ISSUED;
+    } while (0);
+    BDPT_ACTION(act == A_LIGHT_VERTEX) {  // bdpt.h:193-209
         const float dist2 = L.h.dist * L.h.dist;
         const float absCosIn = fabsf(L.h.wo.z);
         L.c.vcm *= (dist2 / absCosIn);
@@ -302,119 +410,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         L.state = ST_SPLAT;
         act = A_ISSUED;
     } while (0);
-    BDPT_ACTION(A_LIGHT_CONTINUE) {  // bdpt.h:211-215
-        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
-        const bool delta = is_delta(b);
-        if (!delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, 1.f);  // the pre-walk vertex state
-        if (!continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray)) {
-            act = A_START_EYE;
-            break;
-        }
-        if (!delta) {
-            L.c.nl++;
-            if (COUNT) cnt.c[4]++;
-        }
-        act = A_LIGHT_NEXT;
-    } while (0);
-    BDPT_ACTION(A_LIGHT_NEXT) {  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
-        if (!(L.c.depth < fr.rr_depth)) {
-            (void)next1(L.rng);
-            act = A_START_EYE;
-        } else {
-            L.state = ST_LIGHT;
-            act = A_ISSUED;
-        }
-    } while (0);
-    BDPT_ACTION(A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
-        const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
-        if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
-            const int mat = __float_as_int(gld4(sc.shade + 5 * static_cast<size_t>(L.c.prim_tri)).w);
-            L.c.Li = ld3(bsdf_of(sc, mat).emission);
-            act = A_FINISH;
-            break;
-        }
-        const float cosCamera = dot(fwd, L.c.cam_d);
-        const float d = fr.cam.vnear / cosCamera;
-        const float t1Pdf = 1.f * (d * d / cosCamera);
-        L.c.tp = mk(1.f, 1.f, 1.f);
-        L.c.vc = 0.f;
-        L.c.vcm = static_cast<float>(fr.W * fr.H) * (1.f / t1Pdf);
-        L.c.depth = 1;
-        L.c.pure = 1u;
-        L.c.Li = mk(0.f, 0.f, 0.f);
-        L.ray = Ray{cam_o, L.c.cam_d, 1.f, 1000.f};
-        act = A_EYE_NEXT;
-        if (1 < fr.rr_depth) {
-            // The eye walk's first intersect (bdpt.h:70) re-traces render()'s
-            // primary ray (bdpt.h:225): same ray, same scene, so the same
-            // (accepted) hit. It is reused instead of traced again.
-            shade_hit(sc, L.c.prim_tri, prim.y, prim.z, prim.x, L.ray.d, L.h);
-            L.c.steps++;
-            act = A_EYE_VERTEX;
-        }
-    } while (0);
-    BDPT_ACTION(A_EYE_VERTEX) {  // bdpt.h:73-150
-        const float dist2 = L.h.dist * L.h.dist;
-        const float absCosIn = fabsf(L.h.wo.z);
-        L.c.vcm *= (dist2 / absCosIn);
-        L.c.vc *= (1.f / absCosIn);
-        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
-        const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
-        if (!is_zero(emission)) {
-            const int eid = shape_emitter_of(sc, L.h.shape);
-            if (eid >= 0) {  // (the reference asserts otherwise, integrator.cpp:56)
-                const EmitterRecord& e = emitter_of(sc, eid);
-                const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
-                if (L.c.depth > 1) {
-                    f3 contrib = ld3(e.radiance) * L.c.tp;
-                    const float pA = 1.f / (e.area * emitterPdf);
-                    const float camW = pA * L.c.vcm + (pA * kInvTwoPi) * L.c.vc;
-                    const float mis = 1.f / (1.f + camW);
-                    if (fr.strategy == 2) {  // PATH_TRACING (bdpt.h:110-113)
-                        if (L.c.pure) L.c.Li = L.c.Li + contrib;
-                    } else {
-                        if (!L.c.pure) contrib = contrib * mis;
-                        L.c.Li = L.c.Li + contrib;
-                    }
-                } else if (L.c.depth == 1) {
-                    L.c.Li = L.c.Li + emission;
-                }
-            }
-            act = A_FINISH;
-            break;
-        }
-        if (is_delta(b)) {
-            act = A_EYE_CONTINUE;
-            break;
-        }
-        L.c.pure = 0u;
-        L.c.ci = 0;
-        act = A_CONN;
-        // connectToLight (bdpt.h:374-430): 4 draws, then everything but visibility.
-        float emitterPdf, posPdf;
-        f3 en, ep;
-        const EmitterRecord& e = sample_emitter(sc, L.rng, emitterPdf, en, ep, posPdf);
-        f3 dir = L.h.p - ep;
-        const float d2 = dot(dir, dir);
-        dir = dir * (1.f / sqrt_cr(d2));
-        const f3 wi = local_at(L.h.n, -dir);
-        const float cosAtLight = dot(en, dir);
-        const float cosAtEye = wi.z;
-        if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
-        const float pdf_w = (emitterPdf * posPdf) * d2 / cosAtLight;
-        const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * (1.f / pdf_w)) * L.c.tp) * ld3(e.radiance);
-        if (is_zero(Li)) break;
-        const float lightWeight = (bsdf_pdf(b, wi, L.h.wo) * 1.f) / pdf_w;
-        const float eyePrevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;
-        const float eyeCurRev_a = cosAtEye * (1.f / d2) * kInvTwoPi;
-        const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
-        const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
-        L.c.pend = (fr.strategy == 0) ? Li * mis : Li;
-        L.ray = shadow_ray(L.h.p, ep);
-        L.state = ST_NEE;
-        act = A_ISSUED;
-    } while (0);
-    BDPT_ACTION(A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
+    BDPT_ACTION(act == A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
         act = A_EYE_CONTINUE;
         if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
         const BsdfRecord& be = bsdf_of(sc, L.h.mat);
@@ -450,11 +446,36 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             break;
         }
     } while (0);
-    BDPT_ACTION(A_EYE_CONTINUE) {  // bdpt.h:152
-        const bool more = continue_walk(bsdf_of(sc, L.h.mat), L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray);
-        act = more ? A_EYE_NEXT : A_FINISH;
+    // ContinuePathRandomWalk of either subpath (light: bdpt.h:211-215, eye: bdpt.h:152).
+    BDPT_ACTION(act == A_LIGHT_CONTINUE || act == A_EYE_CONTINUE) {
+        const bool light = act == A_LIGHT_CONTINUE;
+        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
+        const bool delta = is_delta(b);
+        if (light && !delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, 1.f);  // the pre-walk state
+        const bool more = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray);
+        if (!light) {
+            act = more ? A_EYE_NEXT : A_FINISH;
+        } else if (more) {
+            if (!delta) {
+                L.c.nl++;
+                if (COUNT) cnt.c[4]++;
+            }
+            act = A_LIGHT_NEXT;
+        } else {  // the light subpath ends; the eye subpath starts next step
+            L.state = ST_DEFER;
+            act = A_ISSUED;
+        }
     } while (0);
-    BDPT_ACTION(A_EYE_NEXT) {  // bdpt.h:68
+    BDPT_ACTION(act == A_LIGHT_NEXT) {  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
+        if (!(L.c.depth < fr.rr_depth)) {
+            (void)next1(L.rng);
+            L.state = ST_DEFER;  // the eye subpath starts next step
+        } else {
+            L.state = ST_LIGHT;
+        }
+        act = A_ISSUED;
+    } while (0);
+    BDPT_ACTION(act == A_EYE_NEXT) {  // bdpt.h:68
         if (!(L.c.depth < fr.rr_depth)) {
             (void)next1(L.rng);
             act = A_FINISH;
@@ -463,7 +484,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             act = A_ISSUED;
         }
     } while (0);
-    BDPT_ACTION(A_FINISH) {
+    BDPT_ACTION(act == A_FINISH) {
         finish<COUNT>(L, fr, fb, cnt);
         act = A_DONE;
     } while (0);
@@ -529,11 +550,20 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
             L.c.ci++;
             act = A_CONN;
             break;
+        case ST_DEFER: act = A_START_EYE; break;
         default: act = A_DONE;
     }
     // A state-machine bug must not hang the GPU: bound the queries per sample.
     if (++L.c.steps > kMaxStepsPerSample && act != A_FINISH) act = A_FINISH;
     return act;
+}
+
+// Schedules without an overlapped walk run a deferred action at once.
+template <bool COUNT>
+__device__ __forceinline__ void run_deferred(Lane& L, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
+                                             const LightStore& ls, Counts& cnt) {
+    while (L.state == ST_DEFER)
+        advance<COUNT>(L, resolve<COUNT>(L, -1, 0.f, 0.f, 0.f, sc, fr, fb, cnt), sc, fr, fb, ls, cnt);
 }
 
 __device__ __forceinline__ void flush_counts(const Counts& cnt, unsigned long long* out) {

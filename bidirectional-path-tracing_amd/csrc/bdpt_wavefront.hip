@@ -209,6 +209,7 @@ __global__ __launch_bounds__(kShadeBlock) void bdpt_shade_kernel(const WfParams*
             const LightStore ls = light_store(P.lv, P.fr.rr_depth, s);
             const uint32_t act = resolve<COUNT>(L, __float_as_int(rs.w), rs.x, rs.y, rs.z, P.sc, P.fr, P.fb, cnt);
             advance<COUNT>(L, act, P.sc, P.fr, P.fb, ls, cnt);
+            run_deferred<COUNT>(L, P.sc, P.fr, P.fb, ls, cnt);
         }
     }
     // Slots whose sample is done take the next one.
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(kShadeBlock) void bdpt_shade_kernel(const WfParams*
             if (COUNT) cnt.c[2] += q.nodes, cnt.c[3] += q.tris, cnt.c[15] += q.exact;
             const uint32_t act = resolve<COUNT>(L, q.best, q.t, q.u, q.v, P.sc, P.fr, P.fb, cnt);
             advance<COUNT>(L, act, P.sc, P.fr, P.fb, ls, cnt);
+            run_deferred<COUNT>(L, P.sc, P.fr, P.fb, ls, cnt);
         } while (L.state != ST_IDLE && needs_exact<FULL>(L.ray));
         was_active = true;
     }
