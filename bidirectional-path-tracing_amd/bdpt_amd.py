@@ -34,7 +34,10 @@ REFERENCE_SEED = 260450963  # renderer.cpp:155
 COUNTER_NAMES = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
                  "light_vert_reads", "splats", "rng_draws", "trav_lane_iters", "trav_wave_iters",
                  "shade_lane_actions", "shade_wave_actions", "trav_clocks", "shade_clocks", "loop_clocks",
-                 "slab_fallbacks", "stack_gt8", "stack_gt12", "stack_gt16", "pop_culled"]
+                 "slab_fallbacks", "stack_gt8", "stack_gt12", "stack_gt16", "pop_culled",
+                 "clk_resolve", "clk_start_eye", "clk_eye_vertex", "clk_emitter_sample", "clk_start_light",
+                 "clk_nee", "clk_light_vertex", "clk_connect", "clk_continue", "clk_light_next", "clk_eye_next",
+                 "clk_finish"]
 
 
 class BdptError(RuntimeError):
@@ -60,7 +63,7 @@ class _SceneInfo(ctypes.Structure):
 
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
-                ("counters", ctypes.c_int64 * 20)]
+                ("counters", ctypes.c_int64 * len(COUNTER_NAMES))]  # BDPT_NUM_COUNTERS
 
 
 def build(force: bool = False) -> str:

@@ -17,7 +17,7 @@ constexpr float kInvPi = 0.31830988618379067154f;     // platform.h:51
 constexpr float kInvTwoPi = 0.15915494309189533577f;  // platform.h:52
 constexpr float kEpsilon = 1e-8f;                     // platform.h:56
 constexpr float kTriMinT = 0x1.0624dep-10f;           // smallest float t with (double)t > 1e-3 (accel.h:43)
-constexpr int kCounters = 20;
+constexpr int kCounters = 32;
 #ifndef BDPT_TRAV_WHILE_WHILE
 #define BDPT_TRAV_WHILE_WHILE 1  // megakernel traversal loop shape (0: one node or leaf per iteration)
 #endif
@@ -190,10 +190,10 @@ __device__ __forceinline__ f3 cosine_hemisphere(F2 u) {
         float radius, phi;
         if ((rx * rx) > (ry * ry)) {
             radius = rx;
-            phi = (kPi * 0.25f) * (ry * (1.f / rx));
+            phi = (kPi * 0.25f) * (ry * rcp_cr(rx));
         } else {
             radius = ry;
-            phi = (kPi * 0.5f) - ((kPi * 0.25f) * (rx * (1.f / ry)));
+            phi = (kPi * 0.5f) - ((kPi * 0.25f) * (rx * rcp_cr(ry)));
         }
         const SinCos sc = glibc_sincosf2(phi);
         dx = radius * sc.c;
@@ -225,10 +225,10 @@ __device__ __forceinline__ F2 uniform_triangle(F2 s) {
 // Frame(n) with coordinateSystem (core.h:155-157, math.h:42-51): t = c, s = cross(c, n).
 __device__ __forceinline__ void make_frame(f3 a, f3& s, f3& t) {
     if (fabsf(a.x) > fabsf(a.y)) {
-        float inv = 1.f / sqrt_cr(a.x * a.x + a.z * a.z);
+        float inv = rcp_cr(sqrt_cr(a.x * a.x + a.z * a.z));
         t = mk(a.z * inv, 0.f, -a.x * inv);
     } else {
-        float inv = 1.f / sqrt_cr(a.y * a.y + a.z * a.z);
+        float inv = rcp_cr(sqrt_cr(a.y * a.y + a.z * a.z));
         t = mk(0.f, a.z * inv, -a.y * inv);
     }
     s = cross(t, a);
@@ -287,7 +287,7 @@ struct RayInv {
 };
 __device__ __forceinline__ RayInv ray_inv(const Ray& r) {
     RayInv ri;
-    ri.inv = mk(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+    ri.inv = mk(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
     const float probe = (ri.inv.x + ri.inv.y + ri.inv.z) * 0.f + ((r.o.x + r.o.y + r.o.z) * 0.f);
     ri.fast = (probe == 0.f);  // false iff some component is +-inf or NaN
     return ri;
@@ -343,7 +343,7 @@ __device__ __forceinline__ bool tri_test_edges(f3 v0, f3 e1, f3 e2, const Ray& r
     const f3 pvec = cross(r.d, e2);
     const float det = dot(e1, pvec);
     if (fabsf(det) < kEpsilon) return false;
-    const float invDet = 1.f / det;
+    const float invDet = rcp_det(det);  // |det| >= kEpsilon here
     const f3 tvec = r.o - v0;
     u = dot(tvec, pvec) * invDet;
     if (u < 0.f || u > 1.f) return false;
@@ -812,11 +812,11 @@ __device__ __forceinline__ float bsdf_pdf(const BsdfRecord& b, f3 wi, f3 wo) {
 
 // glass.h:40-53
 __device__ __forceinline__ float fresnel_dielectric(float eta_i, float eta_t, float cos_i, float cos_t) {
-    const float eta = eta_i / eta_t;
+    const float eta = div_cr(eta_i, eta_t);
     const float sin2_t = eta * eta * (glibc_fmaxf(0.f, 1.f - cos_i * cos_i));
     if (sin2_t >= 1.f) return 1.f;
-    const float rpar = ((eta_t * cos_i) - (eta_i * cos_t)) / ((eta_t * cos_i) + (eta_i * cos_t));
-    const float rper = ((eta_i * cos_i) - (eta_t * cos_t)) / ((eta_i * cos_i) + (eta_t * cos_t));
+    const float rpar = div_cr((eta_t * cos_i) - (eta_i * cos_t), (eta_t * cos_i) + (eta_i * cos_t));
+    const float rper = div_cr((eta_i * cos_i) - (eta_t * cos_t), (eta_i * cos_i) + (eta_t * cos_t));
     return (rpar * rpar + rper * rper) * 0.5f;
 }
 
@@ -832,7 +832,7 @@ __device__ BDPT_NOINLINE f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f
             const bool entering = wo.z > 0.f;
             float eta_i = 1.f, eta_t = b.ior;
             if (!entering) { float q = eta_i; eta_i = eta_t; eta_t = q; }
-            const float eta = eta_i / eta_t;
+            const float eta = div_cr(eta_i, eta_t);
             const float sin2_i = glibc_fmaxf(0.f, 1.f - wo.z * wo.z);
             const float sin2_t = eta * eta * sin2_i;
             float cos_t = sqrt_cr(glibc_fmaxf(0.f, 1.f - sin2_t));
@@ -848,14 +848,14 @@ __device__ BDPT_NOINLINE f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f
         case BSDF_MIXTURE: {  // mixture.h:102-151
             f3 val;
             if (u.x < b.specw) {
-                const F2 ns{u.x / b.specw, u.y};
+                const F2 ns{div_cr(u.x, b.specw), u.y};
                 f3 rs, rt;
                 const f3 rn = reflect_z(wo);
                 make_frame(rn, rs, rt);
                 wi = to_world(rs, rt, rn, phong_lobe(ns, b.exponent));
                 val = bsdf_eval(b, wi, wo);
             } else {
-                const F2 ns{(u.x - b.specw) / (1.f - b.specw), u.y};
+                const F2 ns{div_cr(u.x - b.specw, 1.f - b.specw), u.y};
                 wi = cosine_hemisphere(ns);
                 val = bsdf_eval(b, wi, wo);
             }
@@ -920,7 +920,7 @@ __device__ __forceinline__ int sample_emitter(const DevScene& sc, LazyMT& rng, f
     const float w = 1 - uv.x - uv.y;
     pos = (v0 * w + v1 * uv.x) + v2 * uv.y;
     n = normalize((n0 * w + n1 * uv.x) + n2 * uv.y);
-    pos_pdf = 1.f / e.area;
+    pos_pdf = rcp_cr(e.area);
     return static_cast<int>(id);
 }
 

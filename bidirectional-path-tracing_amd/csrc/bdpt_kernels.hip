@@ -162,7 +162,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
         if (has_res) {
             has_res = false;
+            const uint64_t r0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
             const uint32_t act = resolve<COUNT>(L, res, rt, ru, rv, P->sc, P->fr, P->fb, cnt);
+            if (COUNT && first_active_lane()) cnt.c[20] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - r0);
             advance<COUNT>(L, act, P->sc, P->fr, P->fb, ls, cnt);
         }
         if (COUNT && first_active_lane()) {

@@ -91,15 +91,15 @@ __device__ __forceinline__ bool continue_walk(const BsdfRecord& b, const Hit& h,
     pdf *= rrp;
     const float absCosOut = fabsf(wi.z);
     if (is_zero(f)) return false;
-    tp = tp * (f * (1.f / pdf));
+    tp = tp * (f * rcp_cr(pdf));
     depth++;
     const float prevRev = delta ? pdf : bsdf_pdf(b, h.wo, wi) * rrp;  // pdf of the swapped (wo, wi)
     if (delta) {
-        vc = (absCosOut / pdf) * (prevRev * vc);
+        vc = div_cr(absCosOut, pdf) * (prevRev * vc);
         vcm = 0.f;
     } else {
-        vc = (absCosOut / pdf) * (vcm + prevRev * vc);
-        vcm = 1.f / pdf;
+        vc = div_cr(absCosOut, pdf) * (vcm + prevRev * vc);
+        vcm = rcp_cr(pdf);
     }
     ray = Ray{h.p, world_at(h.n, wi), kEpsilon, 3.402823466e+38f};  // FLT_MAX (core.h:120)
     return true;
@@ -118,7 +118,7 @@ __device__ __forceinline__ void splat_pixel(const CameraConstants& c, f3 p, int&
     float b2 = (m[2] * a0 + m[6] * a1) + (m[10] * a2 + m[14] * a3);
     float b3 = (m[3] * a0 + m[7] * a1) + (m[11] * a2 + m[15] * a3);
     const float w = b3;
-    b0 = b0 / w, b1 = b1 / w, b2 = b2 / w, b3 = b3 / w;
+    b0 = div_cr(b0, w), b1 = div_cr(b1, w), b2 = div_cr(b2, w), b3 = div_cr(b3, w);
     m = c.ndc2screen;
     const float d0 = (m[0] * b0 + m[4] * b1) + (m[8] * b2 + m[12] * b3);
     const float d1 = (m[1] * b0 + m[5] * b1) + (m[9] * b2 + m[13] * b3);
@@ -236,9 +236,30 @@ __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __res
 // subpaths. The only edges against this order — a light subpath that ends at its
 // BSDF sample or its depth cap and starts the eye subpath — are deferred to the
 // next shading step (ST_DEFER) instead of being run by a second sweep.
-#define BDPT_ACTION(COND)                     \
+// Counting pass: lanes and wave executions per body ([10], [11]) and wave
+// clocks per body (counters [21 + k]).
+#define BDPT_ACTION(ID, COND)                 \
     if (COUNT) tally_action(cnt, (COND));     \
-    if (COND) do
+    if (COND) do {                            \
+        const ActionClock<COUNT> clk_(cnt, ID);
+#define BDPT_END \
+    }            \
+    while (0)
+template <bool ON>
+struct ActionClock {
+    __device__ ActionClock(Counts&, int) {}
+};
+template <>
+struct ActionClock<true> {
+    Counts& c;
+    int id;
+    uint64_t t0;
+    __device__ ActionClock(Counts& cnt, int i) : c(cnt), id(i), t0(__builtin_amdgcn_s_memtime()) {}
+    __device__ ~ActionClock() {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        if (first_active_lane()) c.c[id] += static_cast<uint32_t>(t1 - t0);
+    }
+};
 __device__ __forceinline__ void tally_action(Counts& cnt, bool on) {
     if (on) {
         cnt.c[10]++;
@@ -251,7 +272,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                         const LightStore& ls, Counts& cnt) {
     const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
     const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
-    BDPT_ACTION(act == A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
+    BDPT_ACTION(21, act == A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
         const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
         if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
             const int mat = __float_as_int(gld4(sc.shade + 5 * static_cast<size_t>(L.c.prim_tri)).w);
@@ -260,11 +281,11 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             break;
         }
         const float cosCamera = dot(fwd, L.c.cam_d);
-        const float d = fr.cam.vnear / cosCamera;
-        const float t1Pdf = 1.f * (d * d / cosCamera);
+        const float d = div_cr(fr.cam.vnear, cosCamera);
+        const float t1Pdf = 1.f * div_cr(d * d, cosCamera);
         L.c.tp = mk(1.f, 1.f, 1.f);
         L.c.vc = 0.f;
-        L.c.vcm = static_cast<float>(fr.W * fr.H) * (1.f / t1Pdf);
+        L.c.vcm = static_cast<float>(fr.W * fr.H) * rcp_cr(t1Pdf);
         L.c.depth = 1;
         L.c.pure = 1u;
         L.c.Li = mk(0.f, 0.f, 0.f);
@@ -278,12 +299,12 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             L.c.steps++;
             act = A_EYE_VERTEX;
         }
-    } while (0);
-    BDPT_ACTION(act == A_EYE_VERTEX) {  // bdpt.h:73-136
+    } BDPT_END;
+    BDPT_ACTION(22, act == A_EYE_VERTEX) {  // bdpt.h:73-136
         const float dist2 = L.h.dist * L.h.dist;
         const float absCosIn = fabsf(L.h.wo.z);
-        L.c.vcm *= (dist2 / absCosIn);
-        L.c.vc *= (1.f / absCosIn);
+        L.c.vcm *= div_cr(dist2, absCosIn);
+        L.c.vc *= rcp_cr(absCosIn);
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
         if (!is_zero(emission)) {
@@ -293,9 +314,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
                 if (L.c.depth > 1) {
                     f3 contrib = ld3(e.radiance) * L.c.tp;
-                    const float pA = 1.f / (e.area * emitterPdf);
+                    const float pA = rcp_cr(e.area * emitterPdf);
                     const float camW = pA * L.c.vcm + (pA * kInvTwoPi) * L.c.vc;
-                    const float mis = 1.f / (1.f + camW);
+                    const float mis = rcp_cr(1.f + camW);
                     if (fr.strategy == 2) {  // PATH_TRACING (bdpt.h:110-113)
                         if (L.c.pure) L.c.Li = L.c.Li + contrib;
                     } else {
@@ -316,16 +337,16 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         L.c.pure = 0u;
         L.c.ci = 0;
         act = A_NEE;
-    } while (0);
+    } BDPT_END;
     // The emitter sample (4 draws) of lightSubpathWalk (bdpt.h:162-163) and of
     // connectToLight (bdpt.h:376-381): selectEmitter + sampleEmitterPosition.
     int e_id = 0;
     float e_pdf = 0.f, e_pos_pdf = 0.f;
     f3 e_n = mk(0.f, 0.f, 0.f), e_p = e_n;
-    BDPT_ACTION(act == A_START_LIGHT || act == A_NEE) {
+    BDPT_ACTION(23, act == A_START_LIGHT || act == A_NEE) {
         e_id = sample_emitter(sc, L.rng, e_pdf, e_n, e_p, e_pos_pdf);
-    } while (0);
-    BDPT_ACTION(act == A_START_LIGHT) {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
+    } BDPT_END;
+    BDPT_ACTION(24, act == A_START_LIGHT) {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
         const EmitterRecord& e = emitter_of(sc, e_id);
         float areaPdf = e_pos_pdf;
         const f3 edir = uniform_hemisphere(next2(L.rng));
@@ -335,9 +356,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         f3 fs, ft;
         make_frame(e_n, fs, ft);
         L.ray = Ray{e_p, to_world(fs, ft, e_n, edir), kEpsilon, 3.402823466e+38f};
-        L.c.tp = (ld3(e.radiance) * edir.z) * (1.f / emissionPdf);
-        L.c.vc = edir.z * (1.f / emissionPdf);
-        L.c.vcm = areaPdf / emissionPdf;
+        L.c.tp = (ld3(e.radiance) * edir.z) * rcp_cr(emissionPdf);
+        L.c.vc = edir.z * rcp_cr(emissionPdf);
+        L.c.vcm = div_cr(areaPdf, emissionPdf);
         L.c.nl = 0;
         L.c.depth = 1;
         if (edir.z <= 0.f) {  // bdpt.h:179-182 (the eye subpath follows)
@@ -346,42 +367,42 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         } else {
             act = A_LIGHT_NEXT;
         }
-    } while (0);
-    BDPT_ACTION(act == A_NEE) {  // connectToLight (bdpt.h:374-430): everything but the visibility test
+    } BDPT_END;
+    BDPT_ACTION(25, act == A_NEE) {  // connectToLight (bdpt.h:374-430): everything but the visibility test
         act = A_CONN;
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         const EmitterRecord& e = emitter_of(sc, e_id);
         f3 dir = L.h.p - e_p;
         const float d2 = dot(dir, dir);
-        dir = dir * (1.f / sqrt_cr(d2));
+        dir = dir * rcp_cr(sqrt_cr(d2));
         const f3 wi = local_at(L.h.n, -dir);
         const float cosAtLight = dot(e_n, dir);
         const float cosAtEye = wi.z;
         if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
-        const float pdf_w = (e_pdf * e_pos_pdf) * d2 / cosAtLight;
-        const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * (1.f / pdf_w)) * L.c.tp) * ld3(e.radiance);
+        const float pdf_w = div_cr((e_pdf * e_pos_pdf) * d2, cosAtLight);
+        const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * rcp_cr(pdf_w)) * L.c.tp) * ld3(e.radiance);
         if (is_zero(Li)) break;
-        const float lightWeight = (bsdf_pdf(b, wi, L.h.wo) * 1.f) / pdf_w;
+        const float lightWeight = div_cr(bsdf_pdf(b, wi, L.h.wo) * 1.f, pdf_w);
         const float eyePrevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;
-        const float eyeCurRev_a = cosAtEye * (1.f / d2) * kInvTwoPi;
+        const float eyeCurRev_a = cosAtEye * rcp_cr(d2) * kInvTwoPi;
         const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
-        const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
+        const float mis = rcp_cr(lightWeight + 1.f + eyeWeight);
         L.c.pend = (fr.strategy == 0) ? Li * mis : Li;
         L.ray = shadow_ray(L.h.p, e_p);
         L.state = ST_NEE;
         act = A_ISSUED;
-    } while (0);
-    BDPT_ACTION(act == A_LIGHT_VERTEX) {  // bdpt.h:193-209
+    } BDPT_END;
+    BDPT_ACTION(26, act == A_LIGHT_VERTEX) {  // bdpt.h:193-209
         const float dist2 = L.h.dist * L.h.dist;
         const float absCosIn = fabsf(L.h.wo.z);
-        L.c.vcm *= (dist2 / absCosIn);
-        L.c.vc *= (1.f / absCosIn);
+        L.c.vcm *= div_cr(dist2, absCosIn);
+        L.c.vc *= rcp_cr(absCosIn);
         act = A_LIGHT_CONTINUE;
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         if (is_delta(b)) break;
         // connectToCamera (bdpt.h:295-371): everything but the visibility test.
         f3 e2l = L.h.p - cam_o;
-        const float invD2 = 1.f / dot(e2l, e2l);
+        const float invD2 = rcp_cr(dot(e2l, e2l));
         e2l = e2l * sqrt_cr(invD2);
         int xp, yp;
         splat_pixel(fr.cam, L.h.p, xp, yp);
@@ -391,26 +412,26 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const f3 wi = local_at(L.h.n, -e2l);
         const f3 f = bsdf_eval(b, wi, L.h.wo);
         if (is_zero(f) || wi.z <= 0.f) break;
-        const float d = fr.cam.vnear / cosCamera;
-        const float img2solid = d * d / cosCamera;
+        const float d = div_cr(fr.cam.vnear, cosCamera);
+        const float img2solid = div_cr(d * d, cosCamera);
         const float img2surf = img2solid * (wi.z * invD2);
-        const float surf2img = 1.f / img2surf;
+        const float surf2img = rcp_cr(img2surf);
         const float nlight = static_cast<float>(fr.W * fr.H);
-        f3 rad = L.c.tp * (f * (1.f / wi.z));
-        rad = rad * (1.f / surf2img);
-        rad = rad * (1.f / nlight);
-        rad = rad * (1.f / static_cast<float>(fr.spp));
+        f3 rad = L.c.tp * (f * rcp_cr(wi.z));
+        rad = rad * rcp_cr(surf2img);
+        rad = rad * rcp_cr(nlight);
+        rad = rad * rcp_cr(static_cast<float>(fr.spp));
         const float reversePdf_a = 1.f * img2surf;
         const float prevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;  // swapped (wi, wo), rr = 1
-        const float lightWeight = (reversePdf_a / nlight) * (L.c.vcm + prevRev * L.c.vc);
-        const float mis = 1.f / (lightWeight + 1.f + 0.f);
+        const float lightWeight = div_cr(reversePdf_a, nlight) * (L.c.vcm + prevRev * L.c.vc);
+        const float mis = rcp_cr(lightWeight + 1.f + 0.f);
         L.c.pend = (fr.strategy == 0) ? rad * mis : rad;
         L.c.pend_px = yp * fr.W + xp;
         L.ray = shadow_ray(cam_o, L.h.p);
         L.state = ST_SPLAT;
         act = A_ISSUED;
-    } while (0);
-    BDPT_ACTION(act == A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
+    } BDPT_END;
+    BDPT_ACTION(27, act == A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
         act = A_EYE_CONTINUE;
         if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
         const BsdfRecord& be = bsdf_of(sc, L.h.mat);
@@ -418,7 +439,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             const Vertex V = load_vertex(ls, L.c.ci);
             if (COUNT) cnt.c[5]++;
             f3 dir = L.h.p - V.p;
-            const float invD2 = 1.f / dot(dir, dir);
+            const float invD2 = rcp_cr(dot(dir, dir));
             dir = dir * sqrt_cr(invD2);
             const f3 wiL = to_local(V.s, V.t, V.n, dir);
             const f3 wiE = local_at(L.h.n, -dir);
@@ -438,16 +459,16 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             const float eyePathRev_a = eyePathRev_w * cosE * invD2;
             const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
             const float eyeWeight = eyePathRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
-            const float mis = 1.f / (lightWeight + 1.f + eyeWeight);
+            const float mis = rcp_cr(lightWeight + 1.f + eyeWeight);
             L.c.pend = Li * mis;
             L.ray = shadow_ray(L.h.p, V.p);
             L.state = ST_CONN;
             act = A_ISSUED;
             break;
         }
-    } while (0);
+    } BDPT_END;
     // ContinuePathRandomWalk of either subpath (light: bdpt.h:211-215, eye: bdpt.h:152).
-    BDPT_ACTION(act == A_LIGHT_CONTINUE || act == A_EYE_CONTINUE) {
+    BDPT_ACTION(28, act == A_LIGHT_CONTINUE || act == A_EYE_CONTINUE) {
         const bool light = act == A_LIGHT_CONTINUE;
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         const bool delta = is_delta(b);
@@ -465,8 +486,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             L.state = ST_DEFER;
             act = A_ISSUED;
         }
-    } while (0);
-    BDPT_ACTION(act == A_LIGHT_NEXT) {  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
+    } BDPT_END;
+    BDPT_ACTION(29, act == A_LIGHT_NEXT) {  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
         if (!(L.c.depth < fr.rr_depth)) {
             (void)next1(L.rng);
             L.state = ST_DEFER;  // the eye subpath starts next step
@@ -474,8 +495,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             L.state = ST_LIGHT;
         }
         act = A_ISSUED;
-    } while (0);
-    BDPT_ACTION(act == A_EYE_NEXT) {  // bdpt.h:68
+    } BDPT_END;
+    BDPT_ACTION(30, act == A_EYE_NEXT) {  // bdpt.h:68
         if (!(L.c.depth < fr.rr_depth)) {
             (void)next1(L.rng);
             act = A_FINISH;
@@ -483,13 +504,14 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             L.state = ST_EYE;
             act = A_ISSUED;
         }
-    } while (0);
-    BDPT_ACTION(act == A_FINISH) {
+    } BDPT_END;
+    BDPT_ACTION(31, act == A_FINISH) {
         finish<COUNT>(L, fr, fb, cnt);
         act = A_DONE;
-    } while (0);
+    } BDPT_END;
 }
 #undef BDPT_ACTION
+#undef BDPT_END
 
 // Starts sample `s` of the shard on this lane: seed, camera ray, primary query.
 __device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame& fr) {

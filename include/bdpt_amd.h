@@ -84,7 +84,7 @@ typedef struct {
     uint32_t flags;        /* BDPT_FLAG_* */
 } bdpt_frame_params;
 
-#define BDPT_NUM_COUNTERS 20
+#define BDPT_NUM_COUNTERS 32
 /* counters: [0] closest-hit rays, [1] shadow rays, [2] interior-node visits,
  * [3] triangle tests, [4] light vertices stored, [5] light-vertex reads,
  * [6] camera splats, [7] RNG draws; SIMD-efficiency probes: [8] traversal
@@ -93,7 +93,11 @@ typedef struct {
  * wave clocks (s_memtime, summed over waves): [12] in traversal, [13] in the
  * state advance, [14] whole persistent loop; [15] exact slab fallbacks;
  * traversal-stack depth probes (after each 4-wide node): [16] entries held
- * beyond depth 8, [17] beyond 12, [18] beyond 16; [19] stack entries culled on pop. */
+ * beyond depth 8, [17] beyond 12, [18] beyond 16; [19] stack entries culled on pop;
+ * wave clocks per state-machine step (megakernel): [20] query resolve, [21] eye start,
+ * [22] eye vertex, [23] emitter sample, [24] light start, [25] next-event estimation,
+ * [26] light vertex + camera connection, [27] vertex connections, [28] BSDF continuation,
+ * [29] light-walk loop test, [30] eye-walk loop test, [31] sample finish. */
 typedef struct {
     double kernel_ms;      /* HIP-event time of the render kernel(s) of the last call */
     int64_t samples;       /* camera samples rendered by the last call */

@@ -34,6 +34,9 @@ out["shade_simd_eff"] = round(c["shade_lane_actions"] / max(64 * c["shade_wave_a
 lc = max(c["loop_clocks"], 1)
 out["trav_clock_frac"] = round(c["trav_clocks"] / lc, 4)
 out["shade_clock_frac"] = round(c["shade_clocks"] / lc, 4)
+clk = {k: v for k, v in c.items() if k.startswith("clk_")}
+tot = max(sum(clk.values()), 1)
+out["shade_split"] = {k[4:]: round(v / tot, 3) for k, v in clk.items()}
 out["kernel_ms"] = round(t_plain, 3)
 out["launches"] = launches
 out["msamples_per_s"] = round(n / t_plain * 1e-3, 3)
