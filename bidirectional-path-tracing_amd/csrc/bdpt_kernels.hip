@@ -32,8 +32,11 @@ constexpr int kBlock = 256;
 #ifndef BDPT_OVERLAP
 #define BDPT_OVERLAP 1  // overlapped walk / shade schedule in the megakernel (0: one query then shade, in lockstep)
 #endif
+#ifndef BDPT_TRAV_SPLIT
+#define BDPT_TRAV_SPLIT 8  // > 0: leaf and interior-node steps in separate iterations (leaf step if 4 * leaf lanes >= SPLIT * node lanes)
+#endif
 #ifndef BDPT_SHADE_READY
-#define BDPT_SHADE_READY 56  // lanes with a finished query that trigger the wave's shading step
+#define BDPT_SHADE_READY 48  // lanes with a finished query that trigger the wave's shading step
 #endif
 
 // One query for the lane's pending state, then the state advance.
@@ -153,7 +156,17 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             if (!tr) break;
             const uint64_t ready = __ballot(has_res);
             if (__popcll(ready) >= BDPT_SHADE_READY) break;
+#if BDPT_TRAV_SPLIT
+            // Lanes at a leaf and lanes at an interior node step in alternate
+            // iterations (whichever group is larger in the sense of the ratio
+            // below) instead of both code paths running in every iteration.
+            const bool at_leaf = (ts.link & kLeafBit) != 0;
+            const uint64_t lv = __ballot(tracing && at_leaf);
+            const bool do_leaf = __popcll(lv) * 4 >= __popcll(tr & ~lv) * BDPT_TRAV_SPLIT;
+            if (tracing && at_leaf == do_leaf && trav_step<COUNT>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
+#else
             if (tracing && trav_step<COUNT>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
+#endif
                 res = ts.best, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;
                 tracing = false;
                 has_res = true;
