@@ -11,6 +11,8 @@ Mirrors the reference's plugin surface for the BDPT path
     .rgb                               Integrator::rgb      (W x H x 3 float32, accumulated)
   Sampler(seed)                        Sampler              src/core/math.h:63-76 (seed + draw count)
   Ray(o, d, min_t, max_t)              Ray                  src/core/core.h:117-122
+  load_toml(path) -> SceneConfig       loadTOML             src/main.cpp:22-116
+  save_exr(rgb, W, H, path)            Integrator::save     integrator.cpp:26-30 -> saveEXR utils.h:95-156
 
 Everything renders on the GPU through the C-ABI of include/bdpt_amd.h; there
 is no CPU fallback (a missing library or device raises).
@@ -61,6 +63,13 @@ class _SceneInfo(ctypes.Structure):
                  "bvh_leaves", "wide_nodes", "wide_depth", "wide_max_stack")]
 
 
+class _Config(ctypes.Structure):  # bdpt_config
+    _fields_ = [("toml_file", ctypes.c_char * 4096), ("obj_file_raw", ctypes.c_char * 4096),
+                ("obj_file", ctypes.c_char * 4096), ("camera", _Camera), ("width", ctypes.c_int32),
+                ("height", ctypes.c_int32), ("realtime", ctypes.c_int32), ("integrator", ctypes.c_char * 32),
+                ("rr_depth", ctypes.c_int32), ("rr_prob", ctypes.c_float), ("spp", ctypes.c_int32)]
+
+
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
                 ("counters", ctypes.c_int64 * len(COUNTER_NAMES))]  # BDPT_NUM_COUNTERS
@@ -99,6 +108,9 @@ def lib():
                                          ctypes.POINTER(i32), f32p, vp]
         L.bdpt_get_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
         L.bdpt_synchronize.argtypes = [vp]
+        L.bdpt_config_load_toml.argtypes = [ctypes.c_char_p, ctypes.POINTER(_Config)]
+        L.bdpt_encode_exr.argtypes = [vp, i32, i32, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+        L.bdpt_save_exr.argtypes = [vp, i32, i32, ctypes.c_char_p]
         _lib = L
     return _lib
 
@@ -139,6 +151,48 @@ class Config:
     rr_prob: float = 0.0  # read but unused: NO_RR = 1 (bdpt.h:18)
     strategy: int = STRATEGY_BDPT
     seed_base: int = REFERENCE_SEED
+
+
+@dataclass
+class SceneConfig:
+    """loadTOML's result (main.cpp:22-116): the scene file settings, plus the
+    objfile resolved as Scene::load does (renderer.cpp:236-241)."""
+    toml_file: str
+    obj_file: str
+    obj_file_raw: str
+    config: Config
+    realtime: bool
+    integrator: str
+
+
+def load_toml(path: str) -> SceneConfig:
+    c = _Config()
+    _check(lib().bdpt_config_load_toml(path.encode(), ctypes.byref(c)))
+    cam = Camera(eye=tuple(c.camera.eye), at=tuple(c.camera.at), up=tuple(c.camera.up), fov=c.camera.fov)
+    cfg = Config(camera=cam, width=c.width, height=c.height, spp=c.spp, rr_depth=c.rr_depth, rr_prob=c.rr_prob)
+    return SceneConfig(toml_file=c.toml_file.decode(), obj_file=c.obj_file.decode(),
+                       obj_file_raw=c.obj_file_raw.decode(), config=cfg, realtime=bool(c.realtime),
+                       integrator=c.integrator.decode())
+
+
+def encode_exr(rgb: np.ndarray, width: int, height: int) -> bytes:
+    """saveEXR's bytes (utils.h:95-156): half-float B, G, R planes, uncompressed."""
+    fb = np.ascontiguousarray(rgb, dtype=np.float32).reshape(-1)
+    if fb.size != width * height * 3:
+        raise BdptError(f"framebuffer has {fb.size} floats, expected {width * height * 3}")
+    n = ctypes.c_int64(0)
+    _check(lib().bdpt_encode_exr(fb.ctypes.data, width, height, None, 0, ctypes.byref(n)))
+    out = np.zeros(n.value, np.uint8)
+    _check(lib().bdpt_encode_exr(fb.ctypes.data, width, height, out.ctypes.data, n.value, ctypes.byref(n)))
+    return out.tobytes()
+
+
+def save_exr(rgb: np.ndarray, width: int, height: int, path: str) -> None:
+    """Integrator::save (integrator.cpp:26-30)."""
+    fb = np.ascontiguousarray(rgb, dtype=np.float32).reshape(-1)
+    if fb.size != width * height * 3:
+        raise BdptError(f"framebuffer has {fb.size} floats, expected {width * height * 3}")
+    _check(lib().bdpt_save_exr(fb.ctypes.data, width, height, path.encode()))
 
 
 @dataclass
@@ -265,3 +319,7 @@ class BDPTIntegrator:
 
     def synchronize(self) -> None:
         _check(lib().bdpt_synchronize(self._h))
+
+    def save(self, path: str) -> None:
+        """Integrator::save: self.rgb as the reference's EXR."""
+        save_exr(self.rgb, self.config.width, self.config.height, path)

@@ -61,6 +61,9 @@ int fail(int code, const std::string& msg) {
 constexpr int kMaxRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
 }  // namespace
 
+// Error reporting shared with the other C-ABI translation units (exr_io.cpp, toml_config.cpp).
+int bdpt::set_error(int code, const std::string& msg) { return fail(code, msg); }
+
 struct bdpt_scene {
     HostScene host;
     DeviceLayout layout;

@@ -78,6 +78,13 @@ struct DeviceLayout {
 
 bool build_device_layout(const HostScene& s, DeviceLayout& out, std::string& err);
 
+// Sets the thread-local message of bdpt_last_error() and returns `code`.
+int set_error(int code, const std::string& msg);
+
+// Integrator::save's EXR (utils.h:95-156 via tinyexr): half-float B, G, R
+// planes, uncompressed scanlines. rgb = W*H*3 floats, pixel-major, row 0 = top.
+bool encode_exr_bgr_half(const float* rgb, int W, int H, std::vector<unsigned char>& out, std::string& err);
+
 // Camera constants (renderer.cpp:140-153, bdpt.h:49-54, :485-489), GLM 0.9.9
 // operation order.
 void camera_constants(const float eye[3], const float at[3], const float up[3], float fov, int width, int height,

@@ -18,6 +18,9 @@
  *   bdpt_render_sample       virtual v3f Integrator::render(const Ray&, Sampler&) const
  *                            src/core/integrator.h:48, overridden at bdpt.h:219
  *   bdpt_ctx_destroy         Integrator/Renderer teardown (renderer.cpp:221-227)
+ *   bdpt_config_load_toml    loadTOML                         src/main.cpp:22-116
+ *   bdpt_save_exr            Integrator::save -> saveEXR      integrator.cpp:26-30, utils.h:95-156
+ *   (CLI lib/tinyrender_amd) main / run                       src/main.cpp:121-181
  *
  * Conventions: plain C types only; status 0 = OK, < 0 = error (message from
  * bdpt_last_error(), thread-local). A context is bound to one HIP device and is
@@ -142,6 +145,35 @@ int bdpt_render_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, const flo
 int bdpt_get_stats(bdpt_ctx* ctx, bdpt_stats* out);
 /* Waits for all work queued by this context (on every stream it was given). */
 int bdpt_synchronize(bdpt_ctx* ctx);
+
+/* ---- scene configuration and image output (host only, no GPU needed) ---- */
+
+/* The settings loadTOML (src/main.cpp:22-116) reads from a scene .toml, with its
+ * defaults and cpptoml's typed-read rules. obj_file is resolved against the
+ * TOML's directory as Scene::load does (renderer.cpp:236-241). */
+typedef struct {
+    char toml_file[4096];
+    char obj_file_raw[4096]; /* [input] objfile as written */
+    char obj_file[4096];     /* resolved path */
+    bdpt_camera camera;      /* [camera] eye / at / up / fov (defaults 1,1,0 / 0,0,0 / 0,1,0 / 30) */
+    int32_t width, height;   /* [film] (defaults 768 x 576) */
+    int32_t realtime;        /* [renderer] realtime (default false) */
+    char integrator[32];     /* [renderer] type (default "normal") */
+    int32_t rr_depth;        /* [renderer] rrDepth (bdpt/path, default 5) */
+    float rr_prob;           /* [renderer] rrProb (bdpt default 0; unused: NO_RR, bdpt.h:18) */
+    int32_t spp;             /* [renderer] spp (default 1) */
+} bdpt_config;
+
+/* loadTOML (main.cpp:22-116). BDPT_ERR_INVALID with the parse error otherwise. */
+int bdpt_config_load_toml(const char* toml_path, bdpt_config* out);
+/* Integrator::save -> saveEXR (integrator.cpp:26-30, utils.h:95-156): the
+ * W*H*3 float framebuffer (pixel-major RGB, row 0 = top) as an uncompressed
+ * scanline OpenEXR with half-float channels B, G, R — byte-identical to the
+ * reference's tinyexr output. bdpt_encode_exr writes into `out` (capacity
+ * bytes; out = NULL only reports *size). */
+int bdpt_encode_exr(const float* rgb, int32_t width, int32_t height, unsigned char* out, int64_t capacity,
+                    int64_t* size);
+int bdpt_save_exr(const float* rgb, int32_t width, int32_t height, const char* path);
 
 #ifdef __cplusplus
 }

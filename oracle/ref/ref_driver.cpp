@@ -19,6 +19,8 @@
 //                   [--row-stride S --row-offset O] [--out fb.f32]
 //   ref_bdpt sample <scene.toml> W H SPP P K      (one sample: Li + splat list)
 //   ref_bdpt dump   <scene.toml> W H OUTDIR       (scene / BVH / camera dump)
+//   ref_bdpt exr    <fb.f32> W H <out.exr>        (the reference's saveEXR, utils.h:95-156)
+//   ref_bdpt toml   <scene.toml>                  (the reference's loadTOML, main.cpp:22-116, as JSON)
 
 #define main tinyrender_reference_main
 #include "main.cpp"   // reference src/main.cpp: loadTOML, g_FrameBufferLocks, tinyobj/tinyexr impl
@@ -289,6 +291,48 @@ int cmdDump(int argc, char** argv) {
     return 0;
 }
 
+// Integrator::save's writer (utils.h:95-156) on a raw float32 framebuffer.
+int cmdExr(int argc, char** argv) {
+    if (argc < 6) return 2;
+    const int W = atoi(argv[3]), H = atoi(argv[4]);
+    std::unique_ptr<v3f[]> rgb(new v3f[size_t(W) * H]);
+    FILE* f = fopen(argv[2], "rb");
+    if (!f) return 1;
+    const size_t n = fread(rgb.get(), sizeof(float), size_t(W) * H * 3, f);
+    fclose(f);
+    if (n != size_t(W) * H * 3) return 1;
+    return saveEXR(rgb, argv[5], W, H) ? 0 : 1;
+}
+
+// loadTOML (main.cpp:22-116) -> the Config fields the BDPT path reads, as JSON.
+int cmdToml(int argc, char** argv) {
+    Config cfg;
+    bool rt;
+    try {
+        rt = loadTOML(cfg, argv[2]);
+    } catch (std::exception const& e) {
+        printf("{\"error\": true}\n");
+        return 0;
+    }
+    const auto& c = cfg.camera;
+    std::string hex;  // objfile bytes as hex (no JSON escaping questions)
+    for (unsigned char ch : cfg.objFile.string()) {
+        char b[3];
+        snprintf(b, sizeof b, "%02x", ch);
+        hex += b;
+    }
+    printf("{\"error\": false, \"objfile_hex\": \"%s\", \"fov\": \"%a\", \"eye\": [\"%a\", \"%a\", \"%a\"], "
+           "\"at\": [\"%a\", \"%a\", \"%a\"], \"up\": [\"%a\", \"%a\", \"%a\"], \"width\": %d, \"height\": %d, "
+           "\"realtime\": %d, \"integrator\": %d",
+           hex.c_str(), c.fov, c.o.x, c.o.y, c.o.z, c.at.x, c.at.y, c.at.z, c.up.x, c.up.y, c.up.z,
+           cfg.width, cfg.height, rt ? 1 : 0, (int)cfg.integrator);
+    if (!rt && (cfg.integrator == EBDPTIntegrator || cfg.integrator == EPathTracerIntegrator))
+        printf(", \"rrDepth\": %d, \"rrProb\": \"%a\"", cfg.integratorSettings.pt.rrDepth, cfg.integratorSettings.pt.rrProb);
+    if (!rt) printf(", \"spp\": %d", cfg.spp);
+    printf("}\n");
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -300,6 +344,8 @@ int main(int argc, char** argv) {
     if (cmd == "render" && argc >= 6) return cmdRender(argc, argv);
     if (cmd == "sample") return cmdSample(argc, argv);
     if (cmd == "dump" && argc >= 6) return cmdDump(argc, argv);
+    if (cmd == "exr") return cmdExr(argc, argv);
+    if (cmd == "toml") return cmdToml(argc, argv);
     fprintf(stderr, "bad command\n");
     return 2;
 }
