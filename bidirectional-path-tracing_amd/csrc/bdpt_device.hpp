@@ -119,16 +119,22 @@ struct LazyMT {
 
 __device__ __forceinline__ uint32_t mt_init_step(uint32_t x, uint32_t i) { return 1812433253u * (x ^ (x >> 30)) + i; }
 
-__device__ __forceinline__ void mt_seed(LazyMT& r, uint32_t seed) {
+// x[397] of the seeding recurrence: the 397 dependent steps (each with a
+// quarter-rate 32-bit multiply) that dominate seeding.
+__device__ __forceinline__ uint32_t mt_x397(uint32_t seed) {
     uint32_t x = seed;
-    r.a0 = x;
-    x = mt_init_step(x, 1);
-    r.a1 = x;
 #pragma unroll 4
-    for (uint32_t i = 2; i <= 397; i++) x = mt_init_step(x, i);
-    r.b = x;
+    for (uint32_t i = 1; i <= 397; i++) x = mt_init_step(x, i);
+    return x;
+}
+// Seeds from a precomputed x[397] (mt_x397(seed)).
+__device__ __forceinline__ void mt_seed_with(LazyMT& r, uint32_t seed, uint32_t x397) {
+    r.a0 = seed;
+    r.a1 = mt_init_step(seed, 1);
+    r.b = x397;
     r.n = 0;
 }
+__device__ __forceinline__ void mt_seed(LazyMT& r, uint32_t seed) { mt_seed_with(r, seed, mt_x397(seed)); }
 
 // Positions the generator after `skip` draws (for Sampler objects that were
 // already advanced, e.g. by the camera jitter of the driver).

@@ -35,6 +35,9 @@ constexpr int kBlock = 256;
 #ifndef BDPT_TRAV_SPLIT
 #define BDPT_TRAV_SPLIT 8  // > 0: leaf and interior-node steps in separate iterations (leaf step if 4 * leaf lanes >= SPLIT * node lanes)
 #endif
+#ifndef BDPT_SEED_CHUNK
+#define BDPT_SEED_CHUNK 1  // refill from per-wave chunks of 64 samples seeded together (0: per-refill seeding)
+#endif
 #ifndef BDPT_SHADE_READY
 #define BDPT_SHADE_READY 48  // lanes with a finished query that trigger the wave's shading step
 #endif
@@ -89,6 +92,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     Lane L(cold_mem[threadIdx.x]);
     L.state = ST_IDLE;
     bool exhausted = false;  // wave-uniform
+#if BDPT_SEED_CHUNK
+    uint64_t chunk_base = 0;  // wave-uniform: the wave's current chunk of samples
+    int chunk_pos = 0, chunk_n = 0;
+    bool global_done = false;
+    uint32_t chunk_x397 = 0;  // lane i: mt_x397 of sample chunk_base + i
+#endif
 #if BDPT_OVERLAP
     const TravScene tsc = trav_scene(kp.sc);
     bool tracing = false, has_res = false, q_any = false;
@@ -106,6 +115,40 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         uint64_t pa = (uint64_t)(ConstKParams)kpp;
         asm volatile("" : "+s"(pa));
         const KParams* P = (const KParams*)(ConstKParams)pa;
+#if BDPT_SEED_CHUNK
+        // Refill idle lanes from the wave's chunk of 64 consecutive samples. A
+        // chunk is claimed with one atomic and the seeding recurrence of all its
+        // samples (mt_x397) runs once with every lane busy, instead of once per
+        // refill with only the refilled lanes doing useful work.
+        while (!exhausted) {
+            const uint64_t idle = __ballot(L.state == ST_IDLE);
+            if (!idle) break;
+            if (chunk_pos >= chunk_n) {
+                if (global_done) {
+                    exhausted = true;
+                    break;
+                }
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(work, 64ull);
+                base = __shfl(base, 0);
+                if (base >= total) {
+                    exhausted = true;
+                    break;
+                }
+                chunk_base = base;
+                chunk_n = static_cast<int>(total - base < 64 ? total - base : 64);
+                chunk_pos = 0;
+                global_done = base + 64 >= total;
+                int px;
+                chunk_x397 = mt_x397(sample_seed(base + lane, P->fr, px));
+            }
+            const int m = min(__popcll(idle), chunk_n - chunk_pos);
+            const int rank = __popcll(idle & ((1ull << lane) - 1ull));
+            const uint32_t x397 = __shfl(chunk_x397, (chunk_pos + rank) & 63);
+            if (L.state == ST_IDLE && rank < m) start_sample<true>(L, chunk_base + chunk_pos + rank, P->fr, x397);
+            chunk_pos += m;
+        }
+#else
         if (!exhausted) {  // refill idle lanes: one atomic per wave
             const uint64_t idle = __ballot(L.state == ST_IDLE);
             if (idle) {
@@ -121,6 +164,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 if (base + n >= total) exhausted = true;
             }
         }
+#endif
         if (__ballot(L.state != ST_IDLE) == 0) {
             if (exhausted) break;
             continue;

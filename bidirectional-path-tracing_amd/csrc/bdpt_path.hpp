@@ -513,15 +513,26 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
 #undef BDPT_ACTION
 #undef BDPT_END
 
-// Starts sample `s` of the shard on this lane: seed, camera ray, primary query.
-__device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame& fr) {
+// Pixel and Sampler seed of sample `s` of the shard: seed_base + p * spp + k
+// (the per-(pixel, sample) convention of SURVEY §8c on renderer.cpp:155).
+__device__ __forceinline__ uint32_t sample_seed(uint64_t s, const DevFrame& fr, int& pixel) {
     const uint64_t per_row = static_cast<uint64_t>(fr.W) * fr.spp;
     const uint64_t lr = s / per_row, q = s % per_row;
     const int j = static_cast<int>(q / fr.spp), k = static_cast<int>(q % fr.spp);
     const int row = fr.row_offset + static_cast<int>(lr) * fr.row_stride;
-    L.c.pixel = row * fr.W + j;
-    mt_seed(L.rng, fr.seed_base + static_cast<uint32_t>(L.c.pixel) * static_cast<uint32_t>(fr.spp) +
-                       static_cast<uint32_t>(k));
+    pixel = row * fr.W + j;
+    return fr.seed_base + static_cast<uint32_t>(pixel) * static_cast<uint32_t>(fr.spp) + static_cast<uint32_t>(k);
+}
+
+// Starts sample `s` of the shard on this lane: seed, camera ray, primary query.
+// x397 = mt_x397(seed) when the caller precomputed it (HAVE_X397).
+template <bool HAVE_X397 = false>
+__device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame& fr, uint32_t x397 = 0) {
+    int pixel;
+    const uint32_t seed = sample_seed(s, fr, pixel);
+    L.c.pixel = pixel;
+    if (HAVE_X397) mt_seed_with(L.rng, seed, x397);
+    else mt_seed(L.rng, seed);
     L.c.cam_d = camera_dir(fr, L.c.pixel, L.rng);
     L.ray = Ray{mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]), L.c.cam_d, 1.f, 1000.f};
     L.c.Li = mk(0.f, 0.f, 0.f);
