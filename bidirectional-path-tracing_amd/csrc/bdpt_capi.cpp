@@ -279,6 +279,19 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
         c->sc.lds_words = up4(c->sc.lds_shape_off + static_cast<uint32_t>(L.shape_emitter.size()));
         if (c->sc.lds_words * 4u > 24u * 1024u)
             return fail(BDPT_ERR_UNSUPPORTED, "BSDF / emitter / shape tables exceed the 24 KiB LDS budget");
+        // Emitter faces + CDFs join the LDS tables when that costs no resident block.
+        c->sc.lds_etri_off = c->sc.lds_ecdf_off = dev::kNoLds;
+        c->sc.n_etri = static_cast<int32_t>(L.emit_tri.size() / 5);
+        c->sc.n_ecdf = static_cast<int32_t>(L.emit_cdf.size());
+        const uint32_t etri = c->sc.lds_words, ecdf = up4(etri + 20u * static_cast<uint32_t>(c->sc.n_etri));
+        const uint32_t with = up4(ecdf + static_cast<uint32_t>(c->sc.n_ecdf));
+        if (with * 4u <= 24u * 1024u &&
+            frame_kernel_blocks_per_cu(4 * static_cast<size_t>(with)) >=
+                frame_kernel_blocks_per_cu(4 * static_cast<size_t>(c->sc.lds_words))) {
+            c->sc.lds_etri_off = etri;
+            c->sc.lds_ecdf_off = ecdf;
+            c->sc.lds_words = with;
+        }
     }
     c->max_depth = s->host.max_depth;
     HIP_TRY(hipMalloc(&c->work, sizeof(unsigned long long)));

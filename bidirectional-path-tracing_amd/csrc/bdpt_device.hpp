@@ -52,7 +52,12 @@ struct DevScene {
     // LDS copy of the small tables (scene_tables_to_lds): word offsets of the
     // emitter records and the shape->emitter map, total words (16-byte rounded)
     uint32_t lds_emit_off, lds_shape_off, lds_words;
+    // emitter faces (5 float4 each) and CDFs, also in LDS when they fit without
+    // costing a resident block (host decision); kNoLds otherwise
+    uint32_t lds_etri_off, lds_ecdf_off;
+    int32_t n_etri, n_ecdf;
 };
+constexpr uint32_t kNoLds = 0xffffffffu;
 
 // Small per-scene tables — BSDF records, emitter records, shape -> emitter
 // map — live in the kernels' dynamic LDS: the divergent shading code reads
@@ -81,6 +86,14 @@ __device__ __forceinline__ void scene_tables_to_lds(const DevScene& sc) {
     for (uint32_t i = threadIdx.x; i < ne; i += blockDim.x) g_scene_lds[sc.lds_emit_off + i] = e[i];
     for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(sc.nshapes); i += blockDim.x)
         g_scene_lds[sc.lds_shape_off + i] = m[i];
+    if (sc.lds_etri_off != kNoLds) {
+        const uint32_t* t = reinterpret_cast<const uint32_t*>(sc.emit_tri);
+        const uint32_t* c = reinterpret_cast<const uint32_t*>(sc.emit_cdf);
+        for (uint32_t i = threadIdx.x; i < 20u * static_cast<uint32_t>(sc.n_etri); i += blockDim.x)
+            g_scene_lds[sc.lds_etri_off + i] = t[i];
+        for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(sc.n_ecdf); i += blockDim.x)
+            g_scene_lds[sc.lds_ecdf_off + i] = c[i];
+    }
     __syncthreads();
 }
 
@@ -908,6 +921,21 @@ __device__ __forceinline__ int cdf_sample(const float* cdf, int ncdf, float u) {
     return i > ncdf - 2 ? ncdf - 2 : i;
 }
 
+// The same search over an LDS copy of the CDF (address space 3: ds_read).
+__device__ __forceinline__ int cdf_sample_lds(const float* cdf_generic, int ncdf, float u) {
+    const __attribute__((address_space(3))) float* cdf =
+        (const __attribute__((address_space(3))) float*)(cdf_generic);
+    int lo = 0, hi = ncdf;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (u < cdf[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    int i = lo - 1;
+    i = i < 0 ? 0 : i;
+    return i > ncdf - 2 ? ncdf - 2 : i;
+}
+
 // selectEmitter + sampleEmitterPosition (integrator.cpp:46-51, :73-100): 4 draws.
 // Returns the emitter index.
 __device__ __forceinline__ int sample_emitter(const DevScene& sc, LazyMT& rng, float& emitter_pdf, f3& n, f3& pos,
@@ -917,10 +945,20 @@ __device__ __forceinline__ int sample_emitter(const DevScene& sc, LazyMT& rng, f
     id = id < static_cast<uint32_t>(sc.nemit - 1) ? id : static_cast<uint32_t>(sc.nemit - 1);
     emitter_pdf = 1.f / static_cast<float>(sc.nemit);
     const EmitterRecord& e = emitter_of(sc, static_cast<int>(id));
-    const int f = cdf_sample(sc.emit_cdf + e.cdf_offset, e.nfaces + 1, next1(rng));
+    const bool lds = sc.lds_etri_off != kNoLds;  // uniform: LDS copies of the faces and CDFs
+    const float* cdf = lds ? reinterpret_cast<const float*>(g_scene_lds + sc.lds_ecdf_off) : sc.emit_cdf;
+    const float u1 = next1(rng);
+    const int f = lds ? cdf_sample_lds(cdf + e.cdf_offset, e.nfaces + 1, u1)
+                      : cdf_sample(cdf + e.cdf_offset, e.nfaces + 1, u1);
     const F2 uv = uniform_triangle(next2(rng));
-    const float4* q = sc.emit_tri + 5 * static_cast<size_t>(e.face_offset + f);
-    const float4 a = q[0], b = q[1], c = q[2], d = q[3], g = q[4];
+    float4 a, b, c, d, g;
+    if (lds) {
+        const float4* q = reinterpret_cast<const float4*>(g_scene_lds + sc.lds_etri_off) + 5 * (e.face_offset + f);
+        a = q[0], b = q[1], c = q[2], d = q[3], g = q[4];
+    } else {
+        const float4* q = sc.emit_tri + 5 * static_cast<size_t>(e.face_offset + f);
+        a = q[0], b = q[1], c = q[2], d = q[3], g = q[4];
+    }
     const f3 v0 = mk(a.x, a.y, a.z), v1 = mk(a.w, b.x, b.y), v2 = mk(b.z, b.w, c.x);
     const f3 n0 = mk(c.y, c.z, c.w), n1 = mk(d.x, d.y, d.z), n2 = mk(d.w, g.x, g.y);
     const float w = 1 - uv.x - uv.y;

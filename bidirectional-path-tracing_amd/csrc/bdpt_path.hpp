@@ -551,7 +551,9 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
     const bool any = is_shadow_state(L.state);
     bool hit = res >= 0;
     if (hit && !any) hit = (t <= L.ray.max_t && t >= L.ray.min_t);  // accel.h:133
-    if (hit && !any) shade_hit(sc, res, u, v, t, L.ray.d, L.h);
+    // The primary hit is shaded later, by the eye walk's first vertex (A_START_EYE
+    // keeps its (t, u, v)); the light walk overwrites L.h before reading it.
+    if (hit && !any && L.state != ST_PRIMARY) shade_hit(sc, res, u, v, t, L.ray.d, L.h);
     uint32_t act;
     switch (L.state) {
         case ST_PRIMARY:
