@@ -27,6 +27,7 @@ class Params(ctypes.Structure):
         ("height", ctypes.c_int),
         ("spp", ctypes.c_int),
         ("rr_depth", ctypes.c_int),
+        ("strategy", ctypes.c_int),  # 0 BDPT, 1 LIGHT_TRACING, 2 PATH_TRACING (bdpt.h:16-17)
     ]
 
 
@@ -70,13 +71,14 @@ def lib():
     return _lib
 
 
-def make_params(cam: dict, width: int, height: int, spp: int, rr_depth: int) -> Params:
+def make_params(cam: dict, width: int, height: int, spp: int, rr_depth: int, strategy: int = 0) -> Params:
     p = Params()
     p.eye[:] = [float(x) for x in cam["eye"]]
     p.at[:] = [float(x) for x in cam["at"]]
     p.up[:] = [float(x) for x in cam["up"]]
     p.fov = float(cam["fov"])
     p.width, p.height, p.spp, p.rr_depth = width, height, spp, rr_depth
+    p.strategy = strategy
     return p
 
 

@@ -26,6 +26,8 @@ typedef struct tro_scene tro_scene;
 typedef struct {
     float eye[3], at[3], up[3], fov;
     int width, height, spp, rr_depth;
+    int strategy; /* 0 BDPT, 1 LIGHT_TRACING, 2 PATH_TRACING (the reference's compile-time
+                     switches, bdpt.h:16-17, as a run-time parameter) */
 } tro_params;
 
 /* Loads an OBJ (+ MTL) exactly as Scene::load does (reference

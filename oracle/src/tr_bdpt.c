@@ -498,6 +498,7 @@ typedef struct {
     m4 w2c, c2clip, ndc2screen;
     float vnear;
     float* fb;
+    int strategy; /* tro_params.strategy */
 } ctx_t;
 
 /* splatToImagePlane (bdpt.h:485-496). static_cast<int> of a NaN or an
@@ -554,7 +555,7 @@ static void connect_to_camera(const ctx_t* c, const pvert_t* lv) {
     float lightWeight = (reversePdf_a / (float)nlight) * (lv->vcm + prevRev * lv->vc);
     float eyeWeight = 0.f;
     float misWeight = 1.f / (lightWeight + 1.f + eyeWeight);
-    radiance = vscale(radiance, misWeight);
+    if (c->strategy == 0) radiance = vscale(radiance, misWeight); /* bdpt.h:355-357 */
     int pixel = yPixel * c->W + xPixel;
     g_ctr[6]++;
     c->fb[3 * (size_t)pixel + 0] += radiance.x;
@@ -595,7 +596,7 @@ static v3 connect_to_light(const ctx_t* c, const pvert_t* ev, tr_sampler* smp) {
     float eyeCurRev_a = cosAtEye * (1.f / d2) * emitterDirectionPdf_w;
     float eyeWeight = eyeCurRev_a * (ev->vcm + eyePrevRev * ev->vc);
     float misWeight = 1.f / (lightWeight + 1.f + eyeWeight);
-    return vscale(Li, misWeight);
+    return c->strategy == 0 ? vscale(Li, misWeight) : Li; /* bdpt.h:426-428 */
 }
 
 /* connectVertices (bdpt.h:434-483) */
@@ -747,8 +748,12 @@ static v3 eye_walk(const ctx_t* c, const pvert_t* lverts, int nl, ray_t ray, tr_
                 float dirPdf = TR_INV_TWOPI;
                 float cameraWeight = pA * vcm + (pA * dirPdf) * vc;
                 float misWeight = 1.f / (1.f + cameraWeight);
-                if (!pureSpecular) contribution = vscale(contribution, misWeight);
-                Li = vadd(Li, contribution);
+                if (c->strategy == 2) { /* PATH_TRACING: pure specular paths only (bdpt.h:110-113) */
+                    if (pureSpecular) Li = vadd(Li, contribution);
+                } else {
+                    if (c->strategy == 0 && !pureSpecular) contribution = vscale(contribution, misWeight); /* :95-99 */
+                    Li = vadd(Li, contribution);
+                }
             } else if (depth == 1) {
                 Li = vadd(Li, emission);
             }
@@ -759,7 +764,8 @@ static v3 eye_walk(const ctx_t* c, const pvert_t* lverts, int nl, ray_t ray, tr_
         if (!is_delta(bsdf_of(s, &hit))) {
             pureSpecular = 0;
             Li = vadd(Li, connect_to_light(c, &ev, smp));
-            for (int i = 0; i < nl; i++) Li = vadd(Li, connect_vertices(c, &lverts[i], &ev));
+            if (c->strategy == 0) /* bdpt.h:145-149 */
+                for (int i = 0; i < nl; i++) Li = vadd(Li, connect_vertices(c, &lverts[i], &ev));
         }
         if (!continue_walk(c, &hit, smp, rrp, &ev, &throughput, &depth, &vc, &vcm, &wi)) break;
     }
@@ -771,6 +777,12 @@ static v3 bdpt_render(const ctx_t* c, ray_t ray, tr_sampler* smp) {
     hit_t hit;
     if (!scene_intersect(c->s, &ray, &hit)) return V3(0, 0, 0);
     pvert_t lverts[MAX_LIGHT_VERTS];
+    if (c->strategy == 1) { /* LIGHT_TRACING (bdpt.h:229-231): light walk, then Le at the primary hit */
+        (void)light_walk(c, smp, lverts);
+        const tro_material* m = &c->s->mats[hit.mat];
+        return V3(m->Ke[0], m->Ke[1], m->Ke[2]);
+    }
+    if (c->strategy == 2) return eye_walk(c, lverts, 0, ray, smp); /* PATH_TRACING (:232-233) */
     int nl = light_walk(c, smp, lverts);
     return eye_walk(c, lverts, nl, ray, smp);
 }
@@ -787,6 +799,7 @@ static void setup(ctx_t* c, camdrv_t* cd, const tro_scene* s, const tro_params* 
     c->H = p->height;
     c->spp = p->spp;
     c->rr_depth = p->rr_depth;
+    c->strategy = p->strategy;
     c->cam_o = V3(p->eye[0], p->eye[1], p->eye[2]);
     tr_camera_mats(p, &c->w2c, &cd->c2w, &c->c2clip, &c->ndc2screen, &cd->angle, &cd->aspect, &c->cam_fwd, &c->vnear);
     cd->invW = 1.f / (float)p->width;

@@ -28,8 +28,10 @@ sys.path.insert(0, os.path.join(REPO, "scenes"))
 import variants  # noqa: E402
 
 REF = os.path.join(REPO, "oracle", "_ref", "ref_bdpt")
+# the reference built with its compile-time strategy switch (bdpt.h:16-17) flipped (oracle/ref/Makefile)
+REF_STRATEGY = {"bdpt": REF, "lt": REF + "_lt", "pt": REF + "_pt"}
 
-# name: (scene, W, H, spp, rrDepth, row_stride)
+# name: (scene, W, H, spp, rrDepth, row_stride[, strategy: bdpt | lt (LIGHT_TRACING) | pt (PATH_TRACING)])
 FRAMEBUFFERS = {
     "G1_cbox_low_64x64_spp4": ("cbox_low", 64, 64, 4, 5, 1),
     "G2_caustic_64x64_spp16": ("caustic", 64, 64, 16, 8, 1),
@@ -41,6 +43,11 @@ FRAMEBUFFERS = {
     "G7_hardlight_512x512_spp4_rows32": ("hardlight", 512, 512, 4, 2, 32),
     # synthetic 1M-triangle box (scenes/synth.py), BASELINE configs[4] at a small size
     "G8_synth1m_48x32_spp2": ("synth1m", 48, 32, 2, 8, 1),
+    # the reference's single-strategy builds (LIGHT_TRACING / PATH_TRACING = 1, bdpt.h:16-17)
+    "G9_caustic_lt_64x64_spp16": ("caustic", 64, 64, 16, 8, 1, "lt"),
+    "G10_caustic_pt_64x64_spp16": ("caustic", 64, 64, 16, 8, 1, "pt"),
+    "G11_hardlight_lt_64x64_spp16": ("hardlight", 64, 64, 16, 2, 1, "lt"),
+    "G12_hardlight_pt_64x64_spp16": ("hardlight", 64, 64, 16, 2, 1, "pt"),
 }
 
 SCENE_DUMPS = {"cbox_low": (64, 64), "caustic": (512, 512), "hardlight": (512, 512), "hardlight_mirror": (512, 512),
@@ -70,14 +77,16 @@ def main() -> None:
         "scenes": dict(old.get("scenes", {})),
     }
     tmp = tempfile.mkdtemp()
-    for name, (scene, W, H, spp, rr, stride) in FRAMEBUFFERS.items():
+    for name, entry in FRAMEBUFFERS.items():
         if only and name not in only:
             continue
+        scene, W, H, spp, rr, stride = entry[:6]
+        strategy = entry[6] if len(entry) > 6 else "bdpt"
         toml = os.path.join(tmp, name + ".toml")
         with open(toml, "w") as f:
             f.write(variants.toml_text(scene, W, H, spp, rr))
         out = os.path.join(tmp, name + ".f32")
-        cmd = [REF, "render", toml, str(W), str(H), str(spp), "--rr", str(rr), "--out", out]
+        cmd = [REF_STRATEGY[strategy], "render", toml, str(W), str(H), str(spp), "--rr", str(rr), "--out", out]
         if stride > 1:
             cmd += ["--row-stride", str(stride)]
         r = subprocess.run(cmd, capture_output=True, text=True, check=True)
@@ -85,6 +94,7 @@ def main() -> None:
         fb = np.fromfile(out, np.float32)
         np.savez_compressed(os.path.join(HERE, name + ".npz"), fb=fb)
         manifest["framebuffers"][name] = dict(scene=scene, width=W, height=H, spp=spp, rr_depth=rr, row_stride=stride,
+                                              strategy=strategy,
                                               samples=info["samples"], sha256=sha(fb.tobytes()),
                                               mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
                                               ref_seconds=info["seconds"])

@@ -21,7 +21,12 @@ TOL = 1e-4
 
 FB_CASES = ["G1_cbox_low_64x64_spp4", "G2_caustic_64x64_spp16", "G3_hardlight_64x64_spp16",
             "G4_hardlight_mirror_64x64_spp16", "G5_caustic_80x48_spp1", "G6_caustic_512x512_spp4_rows16",
-            "G7_hardlight_512x512_spp4_rows32", "G8_synth1m_48x32_spp2"]
+            "G7_hardlight_512x512_spp4_rows32", "G8_synth1m_48x32_spp2",
+            # the reference built with LIGHT_TRACING / PATH_TRACING = 1 (bdpt.h:16-17)
+            "G9_caustic_lt_64x64_spp16", "G10_caustic_pt_64x64_spp16", "G11_hardlight_lt_64x64_spp16",
+            "G12_hardlight_pt_64x64_spp16"]
+STRATEGY = {"bdpt": bdpt_amd.STRATEGY_BDPT, "lt": bdpt_amd.STRATEGY_LIGHT_TRACING,
+            "pt": bdpt_amd.STRATEGY_PATH_TRACING}
 
 _scenes = {}
 
@@ -57,7 +62,7 @@ def report(fb, ref):
 @pytest.mark.parametrize("name", FB_CASES)
 def test_gpu_matches_reference_golden(name, sched, golden_manifest):
     m = golden_manifest["framebuffers"][name]
-    it = integrator(m["scene"], m["width"], m["height"], m["spp"], m["rr_depth"])
+    it = integrator(m["scene"], m["width"], m["height"], m["spp"], m["rr_depth"], STRATEGY[m.get("strategy", "bdpt")])
     fb = it.render_frame(row_offset=0, row_stride=m["row_stride"], flags=sched).reshape(-1)
     assert it.stats()["samples"] == m["samples"]
     ref = load_golden(name)

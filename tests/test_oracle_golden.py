@@ -16,7 +16,11 @@ from conftest import load_golden
 
 FB_CASES = ["G1_cbox_low_64x64_spp4", "G2_caustic_64x64_spp16", "G3_hardlight_64x64_spp16",
             "G4_hardlight_mirror_64x64_spp16", "G5_caustic_80x48_spp1", "G6_caustic_512x512_spp4_rows16",
-            "G7_hardlight_512x512_spp4_rows32", "G8_synth1m_48x32_spp2"]
+            "G7_hardlight_512x512_spp4_rows32", "G8_synth1m_48x32_spp2",
+            # the reference's LIGHT_TRACING / PATH_TRACING builds (bdpt.h:16-17)
+            "G9_caustic_lt_64x64_spp16", "G10_caustic_pt_64x64_spp16", "G11_hardlight_lt_64x64_spp16",
+            "G12_hardlight_pt_64x64_spp16"]
+STRATEGY = {"bdpt": 0, "lt": 1, "pt": 2}
 
 
 @pytest.mark.parametrize("name", FB_CASES)
@@ -24,7 +28,8 @@ def test_oracle_framebuffer_bit_exact(name, golden_manifest):
     meta = golden_manifest["framebuffers"][name]
     sc = variants.SCENES[meta["scene"]]
     scene = O.Scene(variants.obj_path(meta["scene"]))
-    p = O.make_params(sc["camera"], meta["width"], meta["height"], meta["spp"], meta["rr_depth"])
+    p = O.make_params(sc["camera"], meta["width"], meta["height"], meta["spp"], meta["rr_depth"],
+                      STRATEGY[meta.get("strategy", "bdpt")])
     rows = list(range(0, meta["height"], meta["row_stride"]))
     fb, n = scene.render(p, rows=rows)
     assert n == meta["samples"]
