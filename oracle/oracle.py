@@ -28,7 +28,28 @@ class Params(ctypes.Structure):
         ("spp", ctypes.c_int),
         ("rr_depth", ctypes.c_int),
         ("strategy", ctypes.c_int),  # 0 BDPT, 1 LIGHT_TRACING, 2 PATH_TRACING (bdpt.h:16-17)
+        ("integrator", ctypes.c_int),  # 0 BDPTIntegrator, 1 PathTracerIntegrator (path.h)
+        ("pt_explicit", ctypes.c_int),
+        ("pt_max_depth", ctypes.c_int),
+        ("pt_rr_depth", ctypes.c_int),
+        ("pt_rr_prob", ctypes.c_float),
+        ("pt_emitter_samples", ctypes.c_int),
+        ("pt_bsdf_samples", ctypes.c_int),
     ]
+
+
+# [renderer] defaults of a type = "path" scene (main.cpp:96-101)
+PATH_DEFAULTS = dict(explicit=True, max_depth=-1, rr_depth=5, rr_prob=0.95, emitter_samples=1, bsdf_samples=0)
+
+
+def make_path_params(cam: dict, width: int, height: int, spp: int, **path) -> "Params":
+    """Params for PathTracerIntegrator (path.h) with PATH_DEFAULTS overridden by `path`."""
+    s = dict(PATH_DEFAULTS, **path)
+    p = make_params(cam, width, height, spp, s["rr_depth"])
+    p.integrator = 1
+    p.pt_explicit, p.pt_max_depth, p.pt_rr_depth = int(s["explicit"]), s["max_depth"], s["rr_depth"]
+    p.pt_rr_prob, p.pt_emitter_samples, p.pt_bsdf_samples = s["rr_prob"], s["emitter_samples"], s["bsdf_samples"]
+    return p
 
 
 def build(force: bool = False) -> str:

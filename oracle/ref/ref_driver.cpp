@@ -27,6 +27,7 @@
 #undef main
 
 #include <integrators/bdpt.h>
+#include <integrators/path.h>
 #include <bsdfs/mixture.h>
 #include <bsdfs/glass.h>
 
@@ -93,7 +94,8 @@ inline int seedFor(int pixel, int spp, int k) {
 struct Setup {
     Config cfg;
     std::unique_ptr<Scene> scene;
-    std::unique_ptr<BDPTIntegrator> integ;
+    std::unique_ptr<Integrator> integ;  // BDPTIntegrator, or PathTracerIntegrator for TOML type "path"
+    int rrDepth = 0;
 };
 
 void setup(Setup& s, const std::string& toml, int W, int H, int spp, int rr) {
@@ -105,7 +107,11 @@ void setup(Setup& s, const std::string& toml, int W, int H, int spp, int rr) {
     if (rr > 0) s.cfg.integratorSettings.pt.rrDepth = rr;
     s.scene.reset(new Scene(s.cfg));
     if (!s.scene->load(false)) { std::cout.clear(); fprintf(stderr, "scene load failed\n"); exit(2); }
-    s.integ.reset(new BDPTIntegrator(*s.scene));
+    // the offline integrator the TOML names: "bdpt" (the hot path) or "path"
+    // (PathTracerIntegrator, src/integrators/path.h, with its TOML settings)
+    if (s.cfg.integrator == EPathTracerIntegrator) s.integ.reset(new PathTracerIntegrator(*s.scene));
+    else s.integ.reset(new BDPTIntegrator(*s.scene));
+    s.rrDepth = s.cfg.integratorSettings.pt.rrDepth;
     s.integ->init();
     std::cout.clear();
     g_FrameBufferLocks.reset(new std::mutex[(size_t)W * H]);
@@ -164,7 +170,7 @@ int cmdRender(int argc, char** argv) {
         fclose(f);
     }
     printf("{\"samples\": %.0f, \"seconds\": %.6f, \"msamples_per_s\": %.6f, \"threads\": %d, \"rr_depth\": %d}\n",
-           samples, sec, samples / sec * 1e-6, threads, s.integ->m_rrDepth);
+           samples, sec, samples / sec * 1e-6, threads, s.rrDepth);
     return 0;
 }
 

@@ -28,6 +28,12 @@ typedef struct {
     int width, height, spp, rr_depth;
     int strategy; /* 0 BDPT, 1 LIGHT_TRACING, 2 PATH_TRACING (the reference's compile-time
                      switches, bdpt.h:16-17, as a run-time parameter) */
+    /* integrator: 0 BDPTIntegrator (bdpt.h), 1 PathTracerIntegrator (path.h)
+     * with the [renderer] settings of main.cpp:96-101 */
+    int integrator;
+    int pt_explicit, pt_max_depth, pt_rr_depth;
+    float pt_rr_prob;
+    int pt_emitter_samples, pt_bsdf_samples;
 } tro_params;
 
 /* Loads an OBJ (+ MTL) exactly as Scene::load does (reference

@@ -178,8 +178,17 @@ typedef struct {
     v3 p, wo, wi;
     float t;
     int shape, prim, mat;
-    frame_t fs; /* frameNs (frameNg is never read on the BDPT path) */
+    frame_t fs; /* frameNs */
+    v3 ng;      /* frameNg.n (read by the path tracer's BSDF-sampled direct light, path.h:177) */
 } hit_t;
+
+/* A value-initialised SurfaceInteraction (all zero): what the reference's
+ * intersect leaves behind on a miss (matID 0, shapeID 0). */
+static hit_t zero_hit(void) {
+    hit_t h;
+    memset(&h, 0, sizeof h);
+    return h;
+}
 
 static inline v3 tri_v(const tro_scene* s, int t, int c) {
     const float* p = s->tv + 9 * (size_t)t + 3 * c;
@@ -303,6 +312,7 @@ static int scene_intersect(const tro_scene* s, const ray_t* r, hit_t* h) {
     h->shape = s->tshape[tri];
     h->prim = s->tprim[tri];
     h->p = vadd(vadd(vscale(v0, w), vscale(v1, u)), vscale(v2, v));
+    h->ng = vnormalize(vcross(vsub(v1, v0), vsub(v2, v0)));
     h->fs = make_frame(vnormalize(vadd(vadd(vscale(n0, w), vscale(n1, u)), vscale(n2, v))));
     h->wo = to_local(&h->fs, vneg(r->d));
     h->wi = V3(0, 0, 0);
@@ -499,6 +509,7 @@ typedef struct {
     float vnear;
     float* fb;
     int strategy; /* tro_params.strategy */
+    const tro_params* p;
 } ctx_t;
 
 /* splatToImagePlane (bdpt.h:485-496). static_cast<int> of a NaN or an
@@ -787,6 +798,148 @@ static v3 bdpt_render(const ctx_t* c, ray_t ray, tr_sampler* smp) {
     return eye_walk(c, lverts, nl, ray, smp);
 }
 
+/* ------------------------------------------------------------ path tracer */
+/* PathTracerIntegrator (src/integrators/path.h), the other offline integrator
+ * the reference's shipped cbox_bdpt_path.toml selects. */
+static v3 emission_of(const tro_scene* s, const hit_t* h) { /* getEmission (integrator.cpp:41-44) */
+    const tro_material* m = &s->mats[h->mat];
+    return V3(m->Ke[0], m->Ke[1], m->Ke[2]);
+}
+/* balanceHeuristic (path.h:31-34) */
+static float balance_heuristic(float nf, float fPdf, float ng, float gPdf) {
+    float f = nf * fPdf, g = ng * gPdf;
+    return f / (f + g);
+}
+
+/* recursiveImplicit (path.h:36-64). "(1.0 / pdf)" is a double divided and
+ * narrowed to float by glm's scalar operator: the correctly rounded 1.f / pdf. */
+static v3 pt_implicit(const ctx_t* c, tr_sampler* smp, hit_t* hit, int depth) {
+    const tro_scene* s = c->s;
+    if (!(depth < c->p->pt_max_depth)) return V3(0, 0, 0);
+    v2 u = s_next2d(smp);
+    float pdf;
+    v3 f = bsdf_sample(bsdf_of(s, hit), hit, u, &pdf);
+    hit_t vis = zero_hit();
+    v3 wiW = to_world(&hit->fs, hit->wi);
+    ray_t r = {hit->p, wiW, TR_EPSILON, INFINITY};
+    if (!scene_intersect(s, &r, &vis)) return V3(0, 0, 0);
+    float inv = (float)(1.0 / (double)pdf);
+    if (veq0(emission_of(s, &vis))) return vscale(vmul(pt_implicit(c, smp, &vis, depth + 1), f), inv);
+    v3 Li = emission_of(s, &vis);
+    Li = vdot(vis.fs.n, vneg(wiW)) > 0.f ? Li : V3(0, 0, 0);
+    return vscale(vmul(Li, f), inv);
+}
+
+/* recursiveExplicit (path.h:66-202) */
+static v3 pt_explicit(const ctx_t* c, tr_sampler* smp, hit_t* hit, int depth) {
+    const tro_scene* s = c->s;
+    const tro_params* P = c->p;
+    v3 Lr = V3(0, 0, 0);
+    float rrSample = s_next(smp);
+    v3 indirect = V3(0, 0, 0), direct = V3(0, 0, 0);
+    if (depth < P->pt_max_depth || (P->pt_max_depth == -1 && (depth < P->pt_rr_depth || rrSample < P->pt_rr_prob))) {
+        { /* indirect estimator (:77-112): re-sample while an emitter is hit, 0.95 each retry */
+            unsigned nSamples = 0;
+            const float indRRProb = 0.95f;
+            float cumRRProb = 1.f;
+            hit_t vis;
+            int intersects = 0;
+            float pdf = 0.f;
+            v3 f = V3(0, 0, 0);
+            do {
+                vis = zero_hit();
+                v2 u = s_next2d(smp);
+                f = bsdf_sample(bsdf_of(s, hit), hit, u, &pdf);
+                v3 wiW = to_world(&hit->fs, hit->wi);
+                ray_t r = {hit->p, wiW, TR_EPSILON, INFINITY};
+                intersects = scene_intersect(s, &r, &vis);
+                nSamples++;
+            } while (!veq0(emission_of(s, &vis)) && s_next(smp) < indRRProb);
+            cumRRProb = nSamples > 1 ? indRRProb : 1.f;
+            if (intersects && !veq0(f) && veq0(emission_of(s, &vis))) {
+                v3 Li = pt_explicit(c, smp, &vis, depth + 1);
+                indirect = vscale(vscale(vscale(vmul(Li, f), 1.f / pdf), 1.f / (float)nSamples), 1.f / cumRRProb);
+            }
+        }
+        { /* direct estimator (:115-190) */
+            v3 emitterEst = V3(0, 0, 0), bsdfEst = V3(0, 0, 0);
+            for (int i = 0; i < P->pt_emitter_samples; ++i) {
+                float emitterPdf, emitterAreaPdf;
+                v3 nOut, pOut;
+                int id = select_emitter(s, s_next(smp), &emitterPdf);
+                const tro_emitter* e = &s->emit[id];
+                sample_emitter_position(s, smp, e, &nOut, &pOut, &emitterAreaPdf);
+                v3 wiW = vnormalize(vsub(pOut, hit->p));
+                v3 wiLocal = to_local(&hit->fs, wiW);
+                v3 dd = vsub(hit->p, pOut); /* glm::distance2(positionOut, hit.p) */
+                float lightDistanceSquared = vdot(dd, dd);
+                float cosOutgoing = vdot(vneg(wiW), nOut);
+                if (cosOutgoing > 0.f && wiLocal.z > 0.f) {
+                    ray_t r = {hit->p, wiW, TR_EPSILON, INFINITY};
+                    hit_t vis = zero_hit();
+                    if (scene_intersect(s, &r, &vis) && vis.shape == e->shape) {
+                        v3 Li = emission_of(s, &vis);
+                        hit->wi = wiLocal;
+                        float a2s = cosOutgoing * (1.f / lightDistanceSquared);
+                        const tro_bsdf* b = bsdf_of(s, hit);
+                        float bsdfPdf = bsdf_pdf(b, hit);
+                        float w = balance_heuristic((float)P->pt_emitter_samples, emitterAreaPdf * emitterPdf * (1.f / a2s),
+                                                    (float)P->pt_bsdf_samples, bsdfPdf);
+                        v3 t = vmul(vscale(Li, w), bsdf_eval(b, hit));
+                        t = vscale(vscale(vscale(t, 1.f / emitterAreaPdf), 1.f / emitterPdf), a2s);
+                        emitterEst = vadd(emitterEst, t);
+                    }
+                }
+            }
+            emitterEst = P->pt_emitter_samples == 0 ? V3(0, 0, 0) : vdivs(emitterEst, (float)P->pt_emitter_samples);
+            for (int i = 0; i < P->pt_bsdf_samples; ++i) {
+                v2 u = s_next2d(smp);
+                float bsdfPdf;
+                v3 f = bsdf_sample(bsdf_of(s, hit), hit, u, &bsdfPdf);
+                if (veq0(f)) continue;
+                hit_t vis = zero_hit();
+                v3 wiW = to_world(&hit->fs, hit->wi);
+                ray_t r = {hit->p, wiW, TR_EPSILON, INFINITY};
+                if (!scene_intersect(s, &r, &vis)) continue;
+                v3 Li = emission_of(s, &vis);
+                if (veq0(Li)) continue;
+                int eid = s->shape_emitter[vis.shape]; /* getEmitterIDByShapeID (integrator.cpp:53-58) */
+                if (eid < 0) abort();                  /* the reference asserts */
+                const tro_emitter* e = &s->emit[eid];
+                float emitterPdf = 1.f / (float)s->nemit;
+                float emitterAreaPdf = 1.f / e->area;
+                v3 dd = vsub(hit->p, vis.p); /* glm::distance2(vis.p, hit.p) */
+                float lightDistanceSquared = vdot(dd, dd);
+                float cosOutgoing = vdot(vneg(wiW), vis.ng);
+                if (cosOutgoing > 0.f) {
+                    float a2s = cosOutgoing * (1.f / lightDistanceSquared);
+                    float w = balance_heuristic((float)P->pt_bsdf_samples, bsdfPdf, (float)P->pt_emitter_samples,
+                                                emitterPdf * emitterAreaPdf * (1.f / a2s));
+                    bsdfEst = vadd(bsdfEst, vscale(vmul(vscale(Li, w), f), 1.f / bsdfPdf));
+                }
+            }
+            bsdfEst = P->pt_bsdf_samples == 0 ? V3(0, 0, 0) : vdivs(bsdfEst, (float)P->pt_bsdf_samples);
+            direct = vadd(emitterEst, bsdfEst);
+        }
+        Lr = vadd(direct, indirect);
+        if (P->pt_max_depth == -1 && !(depth < P->pt_rr_depth) && (rrSample < P->pt_rr_prob))
+            Lr = vscale(Lr, 1.f / P->pt_rr_prob);
+    }
+    return Lr;
+}
+
+/* PathTracerIntegrator::render (path.h:235-245) with renderExplicit / renderImplicit (:204-233) */
+static v3 pt_render(const ctx_t* c, ray_t ray, tr_sampler* smp) {
+    hit_t hit = zero_hit();
+    if (!scene_intersect(c->s, &ray, &hit)) return V3(0, 0, 0);
+    if (!veq0(emission_of(c->s, &hit))) return emission_of(c->s, &hit);
+    return c->p->pt_explicit ? pt_explicit(c, smp, &hit, 0) : pt_implicit(c, smp, &hit, 0);
+}
+
+static v3 integrator_render(const ctx_t* c, ray_t ray, tr_sampler* smp) {
+    return c->p->integrator == 1 ? pt_render(c, ray, smp) : bdpt_render(c, ray, smp);
+}
+
 /* ------------------------------------------------------------------ driver */
 typedef struct {
     m4 c2w;
@@ -800,6 +953,7 @@ static void setup(ctx_t* c, camdrv_t* cd, const tro_scene* s, const tro_params* 
     c->spp = p->spp;
     c->rr_depth = p->rr_depth;
     c->strategy = p->strategy;
+    c->p = p;
     c->cam_o = V3(p->eye[0], p->eye[1], p->eye[2]);
     tr_camera_mats(p, &c->w2c, &cd->c2w, &c->c2clip, &c->ndc2screen, &cd->angle, &cd->aspect, &c->cam_fwd, &c->vnear);
     cd->invW = 1.f / (float)p->width;
@@ -851,7 +1005,7 @@ int64_t tro_render(const tro_scene* s, const tro_params* p, float* fb, int row_b
             for (int k = 0; k < p->spp; k++) {
                 mt_seed(smp, seed_for(pixel, p->spp, k));
                 ray_t ray = camera_ray(&c, &cd, pixel, smp);
-                acc = vadd(acc, bdpt_render(&c, ray, smp));
+                acc = vadd(acc, integrator_render(&c, ray, smp));
                 n++;
             }
             v3 add = vscale(acc, 1.f / (float)p->spp);
@@ -871,7 +1025,7 @@ void tro_sample(const tro_scene* s, const tro_params* p, int pixel, int k, float
     tr_sampler* smp = (tr_sampler*)malloc(sizeof(tr_sampler));
     mt_seed(smp, seed_for(pixel, p->spp, k));
     ray_t ray = camera_ray(&c, &cd, pixel, smp);
-    v3 L = bdpt_render(&c, ray, smp);
+    v3 L = integrator_render(&c, ray, smp);
     Li[0] = L.x;
     Li[1] = L.y;
     Li[2] = L.z;

@@ -50,6 +50,17 @@ FRAMEBUFFERS = {
     "G12_hardlight_pt_64x64_spp16": ("hardlight", 64, 64, 16, 2, 1, "pt"),
 }
 
+# PathTracerIntegrator (src/integrators/path.h) frames: name: (scene, W, H, spp, path settings)
+PATH_FRAMEBUFFERS = {
+    # the settings of the reference's data/a5/bonus_bdpt/tinyrender/cbox_bdpt_path.toml
+    "P1_hardlight_path_64x64_spp4": ("hardlight", 64, 64, 4, {}),
+    "P2_caustic_path_64x64_spp4": ("caustic", 64, 64, 4, {}),
+    # multiple importance sampling of the direct light (emitter + BSDF samples)
+    "P3_caustic_path_mis_48x48_spp4": ("caustic", 48, 48, 4, dict(emitter_samples=2, bsdf_samples=2)),
+    "P4_cbox_low_path_implicit_64x64_spp4": ("cbox_low", 64, 64, 4, dict(explicit=False, max_depth=5)),
+    "P5_hardlight_path_maxdepth3_48x48_spp4": ("hardlight", 48, 48, 4, dict(max_depth=3, bsdf_samples=1)),
+}
+
 SCENE_DUMPS = {"cbox_low": (64, 64), "caustic": (512, 512), "hardlight": (512, 512), "hardlight_mirror": (512, 512),
                "synth1m": (64, 64)}
 
@@ -99,6 +110,24 @@ def main() -> None:
                                               mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
                                               ref_seconds=info["seconds"])
         print(name, manifest["framebuffers"][name]["sha256"][:16], info)
+    for name, (scene, W, H, spp, path) in PATH_FRAMEBUFFERS.items():
+        if only and name not in only:
+            continue
+        toml = os.path.join(tmp, name + ".toml")
+        with open(toml, "w") as f:
+            f.write(variants.path_toml_text(scene, W, H, spp, **path))
+        out = os.path.join(tmp, name + ".f32")
+        r = subprocess.run([REF, "render", toml, str(W), str(H), str(spp), "--out", out], capture_output=True,
+                           text=True, check=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        fb = np.fromfile(out, np.float32)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), fb=fb)
+        manifest.setdefault("path_framebuffers", dict(old.get("path_framebuffers", {})))
+        manifest["path_framebuffers"][name] = dict(scene=scene, width=W, height=H, spp=spp, path=path,
+                                                   samples=info["samples"], sha256=sha(fb.tobytes()),
+                                                   mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
+                                                   ref_seconds=info["seconds"])
+        print(name, manifest["path_framebuffers"][name]["sha256"][:16], info)
     for scene, (W, H) in SCENE_DUMPS.items():
         if only and scene not in only:
             continue

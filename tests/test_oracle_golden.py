@@ -110,3 +110,21 @@ def test_glibc_mathf_restatement_matches_host_libm():
         for u in us[::5]:
             assert np.float32(L.tro_powf(float(u), float(y))).view(np.uint32) == \
                 np.float32(libm.powf(float(u), float(y))).view(np.uint32)
+
+
+PATH_CASES = ["P1_hardlight_path_64x64_spp4", "P2_caustic_path_64x64_spp4", "P3_caustic_path_mis_48x48_spp4",
+              "P4_cbox_low_path_implicit_64x64_spp4", "P5_hardlight_path_maxdepth3_48x48_spp4"]
+
+
+@pytest.mark.parametrize("name", PATH_CASES)
+def test_oracle_path_tracer_bit_exact(name, golden_manifest):
+    """PathTracerIntegrator (path.h) frames rendered by the reference."""
+    meta = golden_manifest["path_framebuffers"][name]
+    sc = variants.SCENES[meta["scene"]]
+    p = O.make_path_params(sc["camera"], meta["width"], meta["height"], meta["spp"], **meta["path"])
+    fb, n = O.Scene(variants.obj_path(meta["scene"])).render(p)
+    assert n == meta["samples"]
+    ref = load_golden(name)
+    assert hashlib.sha256(ref.tobytes()).hexdigest() == meta["sha256"]
+    mism = np.flatnonzero(fb.view(np.uint32) != ref.view(np.uint32))
+    assert mism.size == 0, f"{mism.size} floats differ, first at {mism[:5]}"
