@@ -12,6 +12,8 @@ Mirrors the reference's plugin surface for the BDPT path
   Sampler(seed)                        Sampler              src/core/math.h:63-76 (seed + draw count)
   Ray(o, d, min_t, max_t)              Ray                  src/core/core.h:117-122
   load_toml(path) -> SceneConfig       loadTOML             src/main.cpp:22-116
+  PathTracerIntegrator(scene, config, PathSettings)
+                                       PathTracerIntegrator src/integrators/path.h (TOML type = "path")
   save_exr(rgb, W, H, path)            Integrator::save     integrator.cpp:26-30 -> saveEXR utils.h:95-156
 
 Everything renders on the GPU through the C-ABI of include/bdpt_amd.h; there
@@ -63,11 +65,17 @@ class _SceneInfo(ctypes.Structure):
                  "bvh_leaves", "wide_nodes", "wide_depth", "wide_max_stack")]
 
 
+class _PathParams(ctypes.Structure):  # bdpt_path_params
+    _fields_ = [("is_explicit", ctypes.c_int32), ("max_depth", ctypes.c_int32), ("rr_depth", ctypes.c_int32),
+                ("rr_prob", ctypes.c_float), ("emitter_samples", ctypes.c_int32), ("bsdf_samples", ctypes.c_int32)]
+
+
 class _Config(ctypes.Structure):  # bdpt_config
     _fields_ = [("toml_file", ctypes.c_char * 4096), ("obj_file_raw", ctypes.c_char * 4096),
                 ("obj_file", ctypes.c_char * 4096), ("camera", _Camera), ("width", ctypes.c_int32),
                 ("height", ctypes.c_int32), ("realtime", ctypes.c_int32), ("integrator", ctypes.c_char * 32),
-                ("rr_depth", ctypes.c_int32), ("rr_prob", ctypes.c_float), ("spp", ctypes.c_int32)]
+                ("rr_depth", ctypes.c_int32), ("rr_prob", ctypes.c_float), ("spp", ctypes.c_int32),
+                ("path", _PathParams)]
 
 
 class _Stats(ctypes.Structure):
@@ -109,6 +117,8 @@ def lib():
         L.bdpt_get_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
         L.bdpt_synchronize.argtypes = [vp]
         L.bdpt_config_load_toml.argtypes = [ctypes.c_char_p, ctypes.POINTER(_Config)]
+        L.bdpt_render_path.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_PathParams), vp, vp]
+        L.bdpt_render_path_host.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_PathParams), vp]
         L.bdpt_encode_exr.argtypes = [vp, i32, i32, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         L.bdpt_save_exr.argtypes = [vp, i32, i32, ctypes.c_char_p]
         _lib = L
@@ -154,6 +164,23 @@ class Config:
 
 
 @dataclass
+class PathSettings:
+    """PathTracerIntegrator settings ([renderer] of a type = "path" scene, main.cpp:96-101)."""
+    explicit: bool = True
+    max_depth: int = -1
+    rr_depth: int = 5
+    rr_prob: float = 0.95
+    emitter_samples: int = 1
+    bsdf_samples: int = 0
+
+    def c(self) -> _PathParams:
+        p = _PathParams()
+        p.is_explicit, p.max_depth, p.rr_depth = int(self.explicit), self.max_depth, self.rr_depth
+        p.rr_prob, p.emitter_samples, p.bsdf_samples = self.rr_prob, self.emitter_samples, self.bsdf_samples
+        return p
+
+
+@dataclass
 class SceneConfig:
     """loadTOML's result (main.cpp:22-116): the scene file settings, plus the
     objfile resolved as Scene::load does (renderer.cpp:236-241)."""
@@ -163,6 +190,7 @@ class SceneConfig:
     config: Config
     realtime: bool
     integrator: str
+    path: PathSettings = field(default_factory=PathSettings)
 
 
 def load_toml(path: str) -> SceneConfig:
@@ -170,9 +198,12 @@ def load_toml(path: str) -> SceneConfig:
     _check(lib().bdpt_config_load_toml(path.encode(), ctypes.byref(c)))
     cam = Camera(eye=tuple(c.camera.eye), at=tuple(c.camera.at), up=tuple(c.camera.up), fov=c.camera.fov)
     cfg = Config(camera=cam, width=c.width, height=c.height, spp=c.spp, rr_depth=c.rr_depth, rr_prob=c.rr_prob)
+    pp = c.path
+    path = PathSettings(explicit=bool(pp.is_explicit), max_depth=pp.max_depth, rr_depth=pp.rr_depth,
+                        rr_prob=pp.rr_prob, emitter_samples=pp.emitter_samples, bsdf_samples=pp.bsdf_samples)
     return SceneConfig(toml_file=c.toml_file.decode(), obj_file=c.obj_file.decode(),
                        obj_file_raw=c.obj_file_raw.decode(), config=cfg, realtime=bool(c.realtime),
-                       integrator=c.integrator.decode())
+                       integrator=c.integrator.decode(), path=path)
 
 
 def encode_exr(rgb: np.ndarray, width: int, height: int) -> bytes:
@@ -323,3 +354,29 @@ class BDPTIntegrator:
     def save(self, path: str) -> None:
         """Integrator::save: self.rgb as the reference's EXR."""
         save_exr(self.rgb, self.config.width, self.config.height, path)
+
+
+class PathTracerIntegrator(BDPTIntegrator):
+    """The reference's PathTracerIntegrator (src/integrators/path.h) on the same
+    GPU substrate: render_frame / render_device as for BDPT (the single-sample
+    render(ray, sampler) entry is BDPT-only)."""
+
+    def __init__(self, scene: Scene, config: Config, path: PathSettings | None = None, device: int = 0):
+        super().__init__(scene, config, device)
+        self.path = path or PathSettings()
+
+    def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:  # noqa: D102
+        raise BdptError("single-sample render(ray, sampler) is only exported for the BDPT integrator")
+
+    def render_frame(self, row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> np.ndarray:
+        if self.rgb is None:
+            self.init()
+        p, pp = self.params(row_offset, row_stride, flags), self.path.c()
+        _check(lib().bdpt_render_path_host(self._h, ctypes.byref(p), ctypes.byref(pp), self.rgb.ctypes.data))
+        return self.rgb
+
+    def render_device(self, fb_ptr: int, stream_ptr: int = 0, row_offset: int = 0, row_stride: int = 1,
+                      flags: int = 0) -> None:
+        p, pp = self.params(row_offset, row_stride, flags), self.path.c()
+        _check(lib().bdpt_render_path(self._h, ctypes.byref(p), ctypes.byref(pp), ctypes.c_void_p(fb_ptr),
+                                      ctypes.c_void_p(stream_ptr)))

@@ -38,6 +38,11 @@ hipError_t wf_launch_pass(const void* dparams, uint32_t flags, uint32_t nslots, 
                           uint32_t p_lds_words, int64_t pass, hipStream_t stream);
 int wf_parts();
 int frame_kernel_blocks_per_cu(size_t dyn_lds);
+size_t pt_params_bytes();
+int pt_blocks_per_cu(size_t dyn_lds);
+hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[7], float* fb,
+                     float4* levels, uint32_t* ring, uint2* gstack, uint32_t nslots, unsigned long long* work,
+                     unsigned long long* counters, int grid, hipStream_t stream, void* dparams);
 int frame_kernel_block();
 int light_vertex_fields();
 }  // namespace bdpt
@@ -107,6 +112,13 @@ struct bdpt_ctx {
     int shade_depth = 0;          // entries the binary traversal can need
     uint32_t* sstack = nullptr;   // overflow beyond shade_lds (scenes deeper than kShadeLdsMax)
     uint32_t sstack_slots = 0;
+    // path tracer (pt_kernels.hip): level stacks, generator rings, parameter block
+    int pt_grid = 0;
+    uint32_t pt_nslots = 0;
+    float4* pt_levels = nullptr;
+    size_t pt_levels_f4 = 0;
+    uint32_t* pt_ring = nullptr;
+    void* pt_dparams = nullptr;
     // stats of the last render
     bool pending_timing = false;
     bdpt_stats stats{};
@@ -219,7 +231,8 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
                     static_cast<void*>(c->gstack), static_cast<void*>(c->wf_lane), static_cast<void*>(c->wf_ray),
                     static_cast<void*>(c->wf_res), static_cast<void*>(c->wf_wctr), static_cast<void*>(c->wf_tctr),
                     static_cast<void*>(c->sstack), c->wf_dparams,
-                    static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams})
+                    static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams,
+                    static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams})
         if (p) (void)hipFree(p);
     if (c->host_ctr) (void)hipHostFree(c->host_ctr);
     for (hipEvent_t e : c->chunk_ev)
@@ -458,6 +471,83 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     c->stats = bdpt_stats{};
     c->stats.samples = static_cast<int64_t>(fr.total_samples);
     c->stats.launches = launches;
+    return BDPT_OK;
+}
+
+static int ensure_tmp_fb(bdpt_ctx* c, size_t floats);
+
+// PathTracerIntegrator (path.h) on the same substrate: pt_kernels.hip.
+constexpr int kPtMaxLevels = 512;  // recursion levels per lane under Russian roulette (P(> 512) ~ 0.95^507)
+
+static int ensure_pt(bdpt_ctx* c, int levels) {
+    if (!c->pt_dparams) {
+        HIP_TRY(hipMalloc(&c->pt_dparams, pt_params_bytes()));
+        // At most 2 resident 256-lane blocks per CU, within the BDPT grid (the
+        // traversal-stack overflow buffer is sized for that many slots).
+        c->pt_grid = std::min(c->grid, c->cus * std::min(2, pt_blocks_per_cu(4 * static_cast<size_t>(c->sc.lds_words))));
+        c->pt_nslots = static_cast<uint32_t>(c->pt_grid) * 256u;
+        HIP_TRY(hipMalloc(&c->pt_ring, sizeof(uint32_t) * 624 * static_cast<size_t>(c->pt_nslots)));
+    }
+    const size_t need = static_cast<size_t>(levels) * 5 * c->pt_nslots;
+    if (need > c->pt_levels_f4) {
+        if (c->pt_levels) HIP_TRY(hipFree(c->pt_levels));
+        c->pt_levels = nullptr;
+        HIP_TRY(hipMalloc(&c->pt_levels, need * sizeof(float4)));
+        c->pt_levels_f4 = need;
+    }
+    return BDPT_OK;
+}
+
+int bdpt_render_path(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_params* path, float* fb,
+                     void* hip_stream) {
+    if (!c || !fb || !path) return fail(BDPT_ERR_INVALID, "null argument");
+    if (!p) return fail(BDPT_ERR_INVALID, "null params");
+    if (p->width <= 0 || p->height <= 0 || p->spp <= 0) return fail(BDPT_ERR_INVALID, "width/height/spp must be > 0");
+    if (static_cast<int64_t>(p->width) * p->height >= (1ll << 31))
+        return fail(BDPT_ERR_INVALID, "image too large (W*H must fit int32, as in the reference)");
+    if (p->row_stride < 1 || p->row_offset < 0) return fail(BDPT_ERR_INVALID, "bad row shard");
+    if (path->emitter_samples < 0 || path->bsdf_samples < 0) return fail(BDPT_ERR_INVALID, "negative sample counts");
+    // the recursion depth the settings allow: maxDepth levels, or Russian roulette
+    const bool rr = path->is_explicit && path->max_depth == -1;
+    const int levels = rr ? kPtMaxLevels : std::max(path->max_depth, 0) + 2;
+    if (levels > kPtMaxLevels) return fail(BDPT_ERR_UNSUPPORTED, "maxDepth > 510 is not supported");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = ensure_pt(c, levels))) return rc;
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    const dev::DevFrame fr = make_frame(p);
+    int32_t settings[7] = {path->is_explicit ? 1 : 0, path->max_depth, path->rr_depth, 0, path->emitter_samples,
+                           path->bsdf_samples, levels};
+    std::memcpy(&settings[3], &path->rr_prob, 4);
+    HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
+    HIP_TRY(hipEventRecord(c->ev0, st));
+    if (fr.total_samples > 0)
+        HIP_TRY(launch_pt(c->sc, fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
+                          c->counters, c->pt_grid, st, c->pt_dparams));
+    HIP_TRY(hipEventRecord(c->ev1, st));
+    c->pending_timing = true;
+    c->stats = bdpt_stats{};
+    c->stats.samples = static_cast<int64_t>(fr.total_samples);
+    c->stats.launches = fr.total_samples > 0 ? 1 : 0;
+    return BDPT_OK;
+}
+
+int bdpt_render_path_host(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_params* path, float* fb_host) {
+    if (!c || !fb_host || !p) return fail(BDPT_ERR_INVALID, "null argument");
+    if (p->width <= 0 || p->height <= 0) return fail(BDPT_ERR_INVALID, "width/height must be > 0");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = static_cast<size_t>(p->width) * p->height * 3;
+    int rc;
+    if ((rc = ensure_tmp_fb(c, n))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->tmp_fb, fb_host, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if ((rc = bdpt_render_path(c, p, path, c->tmp_fb, c->stream))) return rc;
+    HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    bdpt_stats st;
+    if ((rc = bdpt_get_stats(c, &st))) return rc;
+    if (st.counters[1] != 0)
+        return fail(BDPT_ERR_UNSUPPORTED, std::to_string(st.counters[1]) + " samples outgrew the path tracer's level stack");
     return BDPT_OK;
 }
 

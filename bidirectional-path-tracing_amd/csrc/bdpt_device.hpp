@@ -938,7 +938,8 @@ __device__ __forceinline__ int cdf_sample_lds(const float* cdf_generic, int ncdf
 
 // selectEmitter + sampleEmitterPosition (integrator.cpp:46-51, :73-100): 4 draws.
 // Returns the emitter index.
-__device__ __forceinline__ int sample_emitter(const DevScene& sc, LazyMT& rng, float& emitter_pdf, f3& n, f3& pos,
+template <class Rng>
+__device__ __forceinline__ int sample_emitter(const DevScene& sc, Rng& rng, float& emitter_pdf, f3& n, f3& pos,
                                               float& pos_pdf) {
     const float u0 = next1(rng);
     uint32_t id = static_cast<uint32_t>(u0 * static_cast<float>(sc.nemit));

@@ -1,0 +1,522 @@
+// HIP kernel for the reference's other offline integrator, PathTracerIntegrator
+// (src/integrators/path.h): the explicit path tracer (Russian roulette past
+// rrDepth, indirect re-sampling while an emitter is hit, direct light from
+// emitter samples and BSDF samples combined with the balance heuristic) and the
+// implicit one. It runs on the BDPT path's substrate — the same 4-wide
+// traversal with the reference's exact hit semantics, BSDFs, emitter sampling,
+// camera rays and per-(pixel, sample) MT19937 seeding — as a separate
+// persistent kernel, so the BDPT megakernel's register allocation is untouched.
+//
+// The reference recursion (recursiveExplicit calls itself BEFORE computing its
+// own level's direct light, so the random-number order is: level d's Russian
+// roulette and indirect sample(s), then everything below, then level d's
+// direct light) runs as a per-lane state machine with an explicit stack of
+// levels in HBM. Path length is unbounded under Russian roulette, so the
+// generator is the lazy MT19937 of the BDPT path for the first 227 draws and,
+// for the rare longer samples, a 624-word ring of this lane's untempered
+// outputs in HBM (u[n + 624] = u[n + 397] ^ twist(u[n], u[n + 1])).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "bdpt_path.hpp"
+
+namespace bdpt {
+namespace dev {
+
+// ------------------------------------------------------------- generator
+struct PtRng {
+    LazyMT m;          // draws 0 .. 226 need no memory
+    uint32_t seed;
+    uint32_t* ring;    // this lane's 624 words: word k at ring[k * stride]
+    uint32_t stride;
+};
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t v) {
+    v ^= (v >> 11);
+    v ^= (v << 7) & 0x9d2c5680u;
+    v ^= (v << 15) & 0xefc60000u;
+    v ^= (v >> 18);
+    return v;
+}
+__device__ __forceinline__ uint32_t mt_twist(uint32_t a, uint32_t b, uint32_t c) {  // c ^ twist(a, b)
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// Output n >= 227 of std::mt19937(seed): from the ring (and the seeding
+// iterators while n + 1 < 624). The first call materialises outputs 0..226.
+__device__ BDPT_NOINLINE uint32_t pt_u32_slow(PtRng& r) {
+    const uint32_t n = r.m.n;
+    uint32_t* ring = r.ring;
+    const uint32_t st = r.stride;
+    if (n == 227) {
+        LazyMT t;
+        mt_seed(t, r.seed);
+        for (uint32_t k = 0; k < 227; k++) {
+            ring[k * st] = mt_twist(t.a0, t.a1, t.b);
+            t.a0 = t.a1;
+            t.a1 = mt_init_step(t.a1, k + 2);
+            t.b = mt_init_step(t.b, k + 398);
+        }
+    }
+    uint32_t un, un1;
+    if (n < 623) un = r.m.a0, un1 = r.m.a1;
+    else if (n == 623) un = r.m.a0, un1 = ring[0];
+    else un = ring[((n - 624) % 624) * st], un1 = ring[((n - 623) % 624) * st];
+    const uint32_t v = mt_twist(un, un1, ring[((n - 227) % 624) * st]);
+    ring[(n % 624) * st] = v;
+    if (n + 2 <= 623) {
+        r.m.a0 = r.m.a1;
+        r.m.a1 = mt_init_step(r.m.a1, n + 2);
+    } else if (n + 1 <= 623) {
+        r.m.a0 = r.m.a1;
+    }
+    r.m.n = n + 1;
+    return mt_temper(v);
+}
+__device__ __forceinline__ float next1(PtRng& r) {
+    const uint32_t u = r.m.n < 227 ? mt_next_u32(r.m) : pt_u32_slow(r);
+    const float f = static_cast<float>(u) / 4294967296.0f;  // generate_canonical (random.tcc:3348-3380)
+    return f >= 1.0f ? 0x1.fffffep-1f : f;
+}
+__device__ __forceinline__ F2 next2(PtRng& r) {
+    F2 o;
+    o.x = next1(r);
+    o.y = next1(r);
+    return o;
+}
+
+// ------------------------------------------------------------ parameters
+struct PtSettings {
+    int32_t is_explicit, max_depth, rr_depth;
+    float rr_prob;
+    int32_t emitter_samples, bsdf_samples;
+    int32_t max_levels;  // capacity of the level stack
+};
+
+struct PtParams {
+    DevScene sc;
+    DevFrame fr;
+    PtSettings ps;
+    float* fb;
+    float4* levels;       // per slot max_levels x 5 float4
+    uint32_t* ring;       // 624 words per slot, word-major
+    uint2* gstack;        // traversal-stack overflow
+    uint32_t nslots;
+    unsigned long long* work;
+    unsigned long long* counters;  // [0] closest rays (counting pass), [1] level-stack overflows,
+                                   // [2] samples past 227 draws, [3] past 624 draws, [7] RNG draws (counting pass)
+};
+
+enum : uint32_t {  // the query a lane waits on / the step it resumes at
+    PQ_NONE = 0,
+    PQ_PRIMARY,  // render(): primary hit (path.h:238)
+    PQ_IND,      // explicit indirect sample (path.h:90)
+    PQ_DIRE,     // explicit direct light, emitter sample (path.h:134)
+    PQ_DIRB,     // explicit direct light, BSDF sample (path.h:162)
+    PQ_IMP,      // implicit (path.h:43)
+};
+
+struct PtLane {
+    PtRng rng;
+    uint32_t q;  // PQ_*
+    bool busy;
+    Ray ray;
+    Hit h;                      // the current level's vertex
+    int depth, pixel;
+    // current level (explicit)
+    float rr, pdf, cum;
+    uint32_t nsamp;
+    f3 f, ind, eest, best;
+    int i;                      // direct-light sample counter
+    // pending direct-light query
+    int e_shape;
+    float e_cos, e_d2, e_pdf, e_apdf;
+    f3 e_wil, b_f, wiw;
+    float b_pdf;
+};
+
+__device__ __forceinline__ f3 emission_of(const DevScene& sc, int mat) { return ld3(bsdf_of(sc, mat).emission); }
+
+__device__ __forceinline__ float balance_heuristic(float nf, float fPdf, float ng, float gPdf) {  // path.h:31-34
+    const float f = nf * fPdf, g = ng * gPdf;
+    return div_cr(f, f + g);
+}
+
+// Level stack record d of the lane: the level's vertex and its indirect sample.
+__device__ __forceinline__ float4* level_at(const PtParams& P, uint32_t slot, int d) {
+    return P.levels + (static_cast<size_t>(slot) * P.ps.max_levels + static_cast<uint32_t>(d)) * 5;
+}
+__device__ __forceinline__ void push_level(const PtParams& P, uint32_t slot, const PtLane& L) {
+    float4* q = level_at(P, slot, L.depth);
+    gst4(q, make_float4(L.h.p.x, L.h.p.y, L.h.p.z, L.rr));
+    gst4(q + 1, make_float4(L.h.n.x, L.h.n.y, L.h.n.z, L.pdf));
+    gst4(q + 2, make_float4(L.h.wo.x, L.h.wo.y, L.h.wo.z, __int_as_float(L.h.mat)));
+    gst4(q + 3, make_float4(L.f.x, L.f.y, L.f.z, __int_as_float(L.h.shape)));
+    gst4(q + 4, make_float4(__uint_as_float(L.nsamp), L.cum, 0.f, 0.f));
+}
+__device__ __forceinline__ void pop_level(const PtParams& P, uint32_t slot, PtLane& L) {
+    const float4* q = level_at(P, slot, L.depth);
+    const float4 a = gld4(q), b = gld4(q + 1), c = gld4(q + 2), d = gld4(q + 3), e = gld4(q + 4);
+    L.h.p = xyz(a), L.rr = a.w;
+    L.h.n = xyz(b), L.pdf = b.w;
+    L.h.wo = xyz(c), L.h.mat = __float_as_int(c.w);
+    L.f = xyz(d), L.h.shape = __float_as_int(d.w);
+    L.nsamp = __float_as_uint(e.x), L.cum = e.y;
+}
+
+__device__ __forceinline__ Ray pt_ray(f3 o, f3 d) {
+    return Ray{o, d, kEpsilon, __builtin_inff()};  // Ray(hit.p, wiW, Epsilon, infinity)
+}
+
+// Finishes the sample: rgb[p] += Li * (1 / spp) (renderer.cpp:202, one sample at a time).
+__device__ __forceinline__ void pt_finish(PtLane& L, const PtParams& P, f3 Li) {
+    if (Li.x != 0.f || Li.y != 0.f || Li.z != 0.f) {
+        const float inv_spp = 1.f / static_cast<float>(P.fr.spp);
+        float* px = P.fb + 3 * static_cast<size_t>(L.pixel);
+        atomicAdd(px + 0, Li.x * inv_spp);
+        atomicAdd(px + 1, Li.y * inv_spp);
+        atomicAdd(px + 2, Li.z * inv_spp);
+    }
+    if (L.rng.m.n > 227) atomicAdd(P.counters + 2, 1ull);  // the sample ran on the ring generator
+    if (L.rng.m.n > 624) atomicAdd(P.counters + 3, 1ull);  // ... past its first wrap
+    L.busy = false;
+    L.q = PQ_NONE;
+}
+
+enum : int {  // explicit-level steps between queries
+    PS_ENTER,       // recursiveExplicit entry: Russian roulette (path.h:67-74)
+    PS_IND_SAMPLE,  // indirect: sample the BSDF, trace (path.h:86-92)
+    PS_DIRE,        // direct light, next emitter sample (path.h:120-153)
+    PS_DIRB,        // direct light, next BSDF sample (path.h:156-186)
+    PS_LEVEL_DONE,  // Lr = direct + indirect, RR scaling, return (path.h:187-198)
+    PS_RETURN,      // hand Lr to the caller level (path.h:106) or finish the sample
+    PS_IMP_LEVEL,   // recursiveImplicit entry (path.h:36-44)
+    PS_IMP_RETURN,  // Li * brdfCosTheta * (1.0 / pdf) up the implicit recursion
+    PS_WAIT,        // a query was issued
+};
+
+// Runs the lane from step `ps` until it issues a query or finishes its sample.
+__device__ void pt_advance(PtLane& L, int ps, f3 Lr, const PtParams& P, uint32_t slot) {
+    const DevScene& sc = P.sc;
+    const PtSettings& S = P.ps;
+    for (int guard = 0; guard < 1 << 20; guard++) {
+        switch (ps) {
+            case PS_ENTER: {
+                L.rr = next1(L.rng);
+                const bool enter = L.depth < S.max_depth ||
+                                   (S.max_depth == -1 && (L.depth < S.rr_depth || L.rr < S.rr_prob));
+                if (!enter) {
+                    Lr = mk(0.f, 0.f, 0.f);
+                    ps = PS_RETURN;
+                    break;
+                }
+                L.nsamp = 0;
+                L.ind = mk(0.f, 0.f, 0.f);
+                ps = PS_IND_SAMPLE;
+                break;
+            }
+            case PS_IND_SAMPLE: {
+                const F2 u = next2(L.rng);
+                f3 wi;
+                L.f = bsdf_sample(bsdf_of(sc, L.h.mat), L.h.wo, u, wi, L.pdf);
+                L.ray = pt_ray(L.h.p, world_at(L.h.n, wi));
+                L.nsamp++;
+                L.q = PQ_IND;
+                return;
+            }
+            case PS_DIRE: {
+                if (L.i >= S.emitter_samples) {
+                    if (S.emitter_samples != 0) L.eest = L.eest / static_cast<float>(S.emitter_samples);
+                    L.i = 0;
+                    ps = PS_DIRB;
+                    break;
+                }
+                L.i++;
+                float epdf, eapdf;
+                f3 en, ep;
+                const int id = sample_emitter(sc, L.rng, epdf, en, ep, eapdf);
+                const f3 wiW = normalize(ep - L.h.p);
+                const f3 wil = local_at(L.h.n, wiW);
+                const f3 dd = L.h.p - ep;  // glm::distance2(positionOut, hit.p)
+                const float d2 = dot(dd, dd);
+                const float cosOut = dot(-wiW, en);
+                if (cosOut > 0.f && wil.z > 0.f) {
+                    L.e_shape = emitter_of(sc, id).shape;
+                    L.e_cos = cosOut, L.e_d2 = d2, L.e_pdf = epdf, L.e_apdf = eapdf, L.e_wil = wil;
+                    L.ray = pt_ray(L.h.p, wiW);
+                    L.q = PQ_DIRE;
+                    return;
+                }
+                break;  // next emitter sample
+            }
+            case PS_DIRB: {
+                if (L.i >= S.bsdf_samples) {
+                    if (S.bsdf_samples != 0) L.best = L.best / static_cast<float>(S.bsdf_samples);
+                    ps = PS_LEVEL_DONE;
+                    break;
+                }
+                L.i++;
+                const F2 u = next2(L.rng);
+                f3 wi;
+                float pdf;
+                const f3 f = bsdf_sample(bsdf_of(sc, L.h.mat), L.h.wo, u, wi, pdf);
+                if (!is_zero(f)) {
+                    L.b_f = f, L.b_pdf = pdf;
+                    L.wiw = world_at(L.h.n, wi);
+                    L.ray = pt_ray(L.h.p, L.wiw);
+                    L.q = PQ_DIRB;
+                    return;
+                }
+                break;
+            }
+            case PS_LEVEL_DONE: {
+                const f3 direct = L.eest + L.best;
+                Lr = direct + L.ind;
+                if (S.max_depth == -1 && !(L.depth < S.rr_depth) && (L.rr < S.rr_prob)) Lr = Lr * rcp_cr(S.rr_prob);
+                ps = PS_RETURN;
+                break;
+            }
+            case PS_RETURN: {
+                if (L.depth == 0) {
+                    pt_finish(L, P, Lr);
+                    return;
+                }
+                L.depth--;
+                pop_level(P, slot, L);
+                // indirectEstimator = Li * brdfCosTheta * (1/pdf) * (1/nSamples) * (1/cumRRProb) (path.h:106)
+                L.ind = ((Lr * L.f) * rcp_cr(L.pdf)) * rcp_cr(static_cast<float>(L.nsamp));
+                L.ind = L.ind * rcp_cr(L.cum);
+                L.eest = mk(0.f, 0.f, 0.f), L.best = mk(0.f, 0.f, 0.f);
+                L.i = 0;
+                ps = PS_DIRE;
+                break;
+            }
+            case PS_IMP_LEVEL: {
+                if (!(L.depth < S.max_depth)) {
+                    Lr = mk(0.f, 0.f, 0.f);
+                    ps = PS_IMP_RETURN;
+                    break;
+                }
+                const F2 u = next2(L.rng);
+                f3 wi;
+                L.f = bsdf_sample(bsdf_of(sc, L.h.mat), L.h.wo, u, wi, L.pdf);
+                L.wiw = world_at(L.h.n, wi);
+                L.ray = pt_ray(L.h.p, L.wiw);
+                L.q = PQ_IMP;
+                return;
+            }
+            case PS_IMP_RETURN: {
+                if (L.depth == 0) {
+                    pt_finish(L, P, Lr);
+                    return;
+                }
+                L.depth--;
+                pop_level(P, slot, L);
+                Lr = (Lr * L.f) * rcp_cr(L.pdf);  // Li * brdfCosTheta * (1.0 / pdf) (path.h:50, :56)
+                ps = PS_IMP_RETURN;
+                break;
+            }
+            default:
+                return;
+        }
+    }
+    pt_finish(L, P, mk(0.f, 0.f, 0.f));  // unreachable guard
+}
+
+// Applies the closest-hit result of the lane's query and continues.
+template <bool COUNT>
+__device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u, float v, const PtParams& P,
+                                           uint32_t slot, Counts& cnt) {
+    const DevScene& sc = P.sc;
+    const PtSettings& S = P.ps;
+    bool hit = res >= 0 && t <= L.ray.max_t && t >= L.ray.min_t;  // accel.h:133
+    Hit vis;
+    vis.mat = 0, vis.shape = 0;  // a value-initialised SurfaceInteraction on a miss (path.h:84)
+    if (hit) shade_hit(sc, res, u, v, t, L.ray.d, vis);
+    const uint32_t q = L.q;
+    L.q = PQ_NONE;
+    const f3 zero = mk(0.f, 0.f, 0.f);
+    switch (q) {
+        case PQ_PRIMARY: {  // render / renderExplicit / renderImplicit (path.h:204-245)
+            if (!hit) return pt_finish(L, P, zero);
+            const f3 le = emission_of(sc, vis.mat);
+            if (!is_zero(le)) return pt_finish(L, P, le);
+            L.h = vis;
+            L.depth = 0;
+            return pt_advance(L, S.is_explicit ? PS_ENTER : PS_IMP_LEVEL, zero, P, slot);
+        }
+        case PQ_IND: {  // the do-while of path.h:82-95 and the recursion test of :98-108
+            const bool emitter = !is_zero(emission_of(sc, vis.mat));
+            if (emitter && next1(L.rng) < 0.95f) return pt_advance(L, PS_IND_SAMPLE, zero, P, slot);
+            L.cum = L.nsamp > 1 ? 0.95f : 1.f;
+            L.eest = zero, L.best = zero;
+            L.i = 0;
+            if (hit && !is_zero(L.f) && !emitter) {
+                if (L.depth + 1 >= S.max_levels) {  // out of level stack: flagged, the sample ends
+                    atomicAdd(P.counters + 1, 1ull);
+                    return pt_finish(L, P, zero);
+                }
+                push_level(P, slot, L);
+                L.h = vis;
+                L.depth++;
+                return pt_advance(L, PS_ENTER, zero, P, slot);
+            }
+            return pt_advance(L, PS_DIRE, zero, P, slot);  // no recursion: indirectEstimator stays 0
+        }
+        case PQ_DIRE: {  // path.h:134-151
+            if (hit && vis.shape == L.e_shape) {
+                const f3 Li = emission_of(sc, vis.mat);
+                const BsdfRecord& b = bsdf_of(sc, L.h.mat);
+                const float a2s = L.e_cos * rcp_cr(L.e_d2);
+                const float bsdfPdf = bsdf_pdf(b, L.e_wil, L.h.wo);
+                const float w = balance_heuristic(static_cast<float>(S.emitter_samples),
+                                                  (L.e_apdf * L.e_pdf) * rcp_cr(a2s),
+                                                  static_cast<float>(S.bsdf_samples), bsdfPdf);
+                f3 c = (Li * w) * bsdf_eval(b, L.e_wil, L.h.wo);
+                c = ((c * rcp_cr(L.e_apdf)) * rcp_cr(L.e_pdf)) * a2s;
+                L.eest = L.eest + c;
+            }
+            return pt_advance(L, PS_DIRE, zero, P, slot);
+        }
+        case PQ_DIRB: {  // path.h:162-184
+            if (hit) {
+                const f3 Li = emission_of(sc, vis.mat);
+                const int eid = shape_emitter_of(sc, vis.shape);
+                if (!is_zero(Li) && eid >= 0) {
+                    const EmitterRecord& e = emitter_of(sc, eid);
+                    const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
+                    const float emitterAreaPdf = rcp_cr(e.area);
+                    const f3 dd = L.h.p - vis.p;  // glm::distance2(visibilityInteraction.p, hit.p)
+                    const float d2 = dot(dd, dd);
+                    const f3 e1 = xyz(gld4(sc.tri + 3 * static_cast<size_t>(res) + 1));
+                    const f3 e2 = xyz(gld4(sc.tri + 3 * static_cast<size_t>(res) + 2));
+                    const f3 ng = normalize(cross(e1, e2));  // frameNg.n (accel.h:162)
+                    const float cosOut = dot(-L.wiw, ng);
+                    if (cosOut > 0.f) {
+                        const float a2s = cosOut * rcp_cr(d2);
+                        const float w = balance_heuristic(static_cast<float>(S.bsdf_samples), L.b_pdf,
+                                                          static_cast<float>(S.emitter_samples),
+                                                          (emitterPdf * emitterAreaPdf) * rcp_cr(a2s));
+                        L.best = L.best + ((Li * w) * L.b_f) * rcp_cr(L.b_pdf);
+                    }
+                }
+            }
+            return pt_advance(L, PS_DIRB, zero, P, slot);
+        }
+        case PQ_IMP: {  // path.h:45-59
+            if (!hit) return pt_advance(L, PS_IMP_RETURN, zero, P, slot);
+            const f3 le = emission_of(sc, vis.mat);
+            if (is_zero(le)) {
+                if (L.depth + 1 >= S.max_levels) {
+                    atomicAdd(P.counters + 1, 1ull);
+                    return pt_finish(L, P, zero);
+                }
+                push_level(P, slot, L);
+                L.h = vis;
+                L.depth++;
+                return pt_advance(L, PS_IMP_LEVEL, zero, P, slot);
+            }
+            const f3 Li = dot(vis.n, -L.wiw) > 0.f ? le : zero;
+            return pt_advance(L, PS_IMP_RETURN, (Li * L.f) * rcp_cr(L.pdf), P, slot);
+        }
+        default: return;
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(256) void pt_frame_kernel(const PtParams* __restrict__ pp) {
+    const PtParams& P = *pp;
+    __shared__ uint2 stack_mem[kLdsStack * 256];
+    scene_tables_to_lds(P.sc);
+    const uint32_t slot = blockIdx.x * 256 + threadIdx.x;
+    const Stack stk{stack_mem + threadIdx.x, 256, kLdsStack, P.gstack, P.nslots, slot};
+    const int lane = threadIdx.x & 63;
+    Counts cnt;
+    for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
+    PtLane L;
+    L.busy = false;
+    L.q = PQ_NONE;
+    L.rng.ring = P.ring + slot;
+    L.rng.stride = P.nslots;
+    const uint64_t total = P.fr.total_samples;
+    bool exhausted = false;
+    for (;;) {
+        if (!exhausted) {  // refill idle lanes: one atomic per wave
+            const uint64_t idle = __ballot(!L.busy);
+            if (idle) {
+                const int n = __popcll(idle);
+                const int leader = __ffsll(static_cast<unsigned long long>(idle)) - 1;
+                unsigned long long base = 0;
+                if (lane == leader) base = atomicAdd(P.work, static_cast<unsigned long long>(n));
+                base = __shfl(base, leader);
+                if (!L.busy) {
+                    const uint64_t s = base + __popcll(idle & ((1ull << lane) - 1ull));
+                    if (s < total) {
+                        L.rng.seed = sample_seed(s, P.fr, L.pixel);
+                        mt_seed(L.rng.m, L.rng.seed);
+                        const f3 d = camera_dir(P.fr, L.pixel, L.rng.m);  // draws 0, 1 (< 227)
+                        L.ray = Ray{mk(P.fr.cam_o[0], P.fr.cam_o[1], P.fr.cam_o[2]), d, 1.f, 1000.f};
+                        L.q = PQ_PRIMARY;
+                        L.busy = true;
+                    }
+                }
+                if (base + n >= total) exhausted = true;
+            }
+        }
+        if (__ballot(L.busy) == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        if (L.busy) {
+            if (COUNT) cnt.c[0]++;
+            float t = 0.f, u = 0.f, v = 0.f;
+            const int res = traverse<false, COUNT>(P.sc, L.ray, false, stk, t, u, v, cnt);
+            pt_resolve<COUNT>(L, res, t, u, v, P, slot, cnt);
+            if (COUNT && !L.busy) cnt.c[7] += L.rng.m.n;
+        }
+    }
+    if (COUNT) flush_counts(cnt, P.counters);
+}
+
+}  // namespace dev
+
+// ------------------------------------------------------------ host side
+size_t pt_params_bytes() { return sizeof(dev::PtParams); }
+int pt_block() { return 256; }
+int pt_lds_stack() { return dev::kLdsStack; }
+
+int pt_blocks_per_cu(size_t dyn_lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pt_frame_kernel<false>, 256, dyn_lds) != hipSuccess ||
+        n <= 0)
+        n = 1;
+    return n;
+}
+
+hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[7], float* fb,
+                     float4* levels, uint32_t* ring, uint2* gstack, uint32_t nslots, unsigned long long* work,
+                     unsigned long long* counters, int grid, hipStream_t stream, void* dparams) {
+    dev::PtParams host{};
+    host.sc = sc;
+    host.fr = fr;
+    host.ps.is_explicit = settings[0];
+    host.ps.max_depth = settings[1];
+    host.ps.rr_depth = settings[2];
+    std::memcpy(&host.ps.rr_prob, &settings[3], 4);
+    host.ps.emitter_samples = settings[4];
+    host.ps.bsdf_samples = settings[5];
+    host.ps.max_levels = settings[6];
+    host.fb = fb, host.levels = levels, host.ring = ring, host.gstack = gstack, host.nslots = nslots;
+    host.work = work, host.counters = counters;
+    hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    const dev::PtParams* kp = static_cast<const dev::PtParams*>(dparams);
+    const size_t lds = 4 * static_cast<size_t>(sc.lds_words);
+    if (fr.flags & 1u) hipLaunchKernelGGL((dev::pt_frame_kernel<true>), dim3(grid), dim3(256), lds, stream, kp);
+    else hipLaunchKernelGGL((dev::pt_frame_kernel<false>), dim3(grid), dim3(256), lds, stream, kp);
+    return hipGetLastError();
+}
+
+}  // namespace bdpt

@@ -4,7 +4,8 @@
 // (main.cpp:146-152, "Render took: ... seconds.") -> Integrator::save, which
 // writes the EXR next to the TOML (integrator.cpp:26-30).
 //
-// Only what the GPU path covers is accepted: offline `type = "bdpt"`. Other
+// Offline `type = "bdpt"` (the hot path) and `type = "path"` (the reference's
+// PathTracerIntegrator on the same substrate) are accepted; the other
 // integrators and the realtime render passes are rejected with an error.
 // Optional overrides (not in the reference): --width W --height H --spp N
 // --rr D --device K --out FILE.exr --seed S.
@@ -79,7 +80,8 @@ int main(int argc, char** argv) {
         return EXIT_FAILURE;
     }
     std::printf("%s\n", cfg.integrator);  // main.cpp:72
-    if (std::strcmp(cfg.integrator, "bdpt") != 0) {
+    const bool path = std::strcmp(cfg.integrator, "path") == 0;
+    if (!path && std::strcmp(cfg.integrator, "bdpt") != 0) {
         std::fprintf(stderr, "integrator type \"%s\" is not part of the MI355X BDPT path\n", cfg.integrator);
         return EXIT_FAILURE;
     }
@@ -107,7 +109,13 @@ int main(int argc, char** argv) {
     std::vector<float> rgb(static_cast<size_t>(cfg.width) * cfg.height * 3, 0.f);  // Integrator::init: rgb->clear()
 
     const auto t0 = std::chrono::high_resolution_clock::now();
-    if (bdpt_render_host(ctx, &p, rgb.data()) != BDPT_OK) return die("bdpt_render_host");
+    if (path) {
+        if (rr > 0) cfg.path.rr_depth = rr;
+        p.rr_depth = 1;  // unused by the path tracer
+        if (bdpt_render_path_host(ctx, &p, &cfg.path, rgb.data()) != BDPT_OK) return die("bdpt_render_path_host");
+    } else if (bdpt_render_host(ctx, &p, rgb.data()) != BDPT_OK) {
+        return die("bdpt_render_host");
+    }
     const auto t1 = std::chrono::high_resolution_clock::now();
     std::printf("Render took: %g seconds.\n", std::chrono::duration<double>(t1 - t0).count());
 

@@ -431,6 +431,7 @@ bool load_toml_config(const std::string& path, bdpt_config& cfg, std::string& er
     cfg.rr_depth = 5;
     cfg.rr_prob = 0.f;
     cfg.spp = 1;
+    cfg.path = bdpt_path_params{1, -1, 5, 0.95f, 1, 0};
     if (!cfg.realtime) {
         const std::string t = cfg.integrator;
         static const char* known[] = {"normal", "simple", "ao", "ro", "direct", "path", "bdpt"};
@@ -443,9 +444,21 @@ bool load_toml_config(const std::string& path, bdpt_config& cfg, std::string& er
         if (t == "bdpt") {  // main.cpp:103-107
             if (!get_int(renderer, "rrDepth", 5, cfg.rr_depth, err)) return false;
             cfg.rr_prob = static_cast<float>(get_double(renderer, "rrProb", 0.f));
-        } else if (t == "path") {  // main.cpp:96-99 (rrDepth / rrProb of the path tracer)
+        } else if (t == "path") {  // main.cpp:96-101
             if (!get_int(renderer, "rrDepth", 5, cfg.rr_depth, err)) return false;
             cfg.rr_prob = static_cast<float>(get_double(renderer, "rrProb", 0.95f));
+            cfg.path.is_explicit = get_bool(renderer, "isExplicit", true) ? 1 : 0;
+            if (!get_int(renderer, "maxDepth", -1, cfg.path.max_depth, err)) return false;
+            // get_as<size_t>: a negative integer throws (cpptoml.h:1245-1262)
+            if (!get_int(renderer, "emitterSamples", 1, cfg.path.emitter_samples, err) ||
+                !get_int(renderer, "bsdfSamples", 0, cfg.path.bsdf_samples, err))
+                return false;
+            if (cfg.path.emitter_samples < 0 || cfg.path.bsdf_samples < 0) {
+                err = "T cannot store negative value in get";
+                return false;
+            }
+            cfg.path.rr_depth = cfg.rr_depth;
+            cfg.path.rr_prob = cfg.rr_prob;
         }
         if (!get_int(renderer, "spp", 1, cfg.spp, err)) return false;  // main.cpp:112
     }

@@ -21,6 +21,9 @@
  *   bdpt_config_load_toml    loadTOML                         src/main.cpp:22-116
  *   bdpt_save_exr            Integrator::save -> saveEXR      integrator.cpp:26-30, utils.h:95-156
  *   (CLI lib/tinyrender_amd) main / run                       src/main.cpp:121-181
+ *   bdpt_render_path         PathTracerIntegrator::render     src/integrators/path.h:235-245 for every
+ *                            (pixel, sample) of the offline loop (the reference's other offline
+ *                            integrator, TOML type = "path"), on the same GPU substrate
  *
  * Conventions: plain C types only; status 0 = OK, < 0 = error (message from
  * bdpt_last_error(), thread-local). A context is bound to one HIP device and is
@@ -146,6 +149,28 @@ int bdpt_get_stats(bdpt_ctx* ctx, bdpt_stats* out);
 /* Waits for all work queued by this context (on every stream it was given). */
 int bdpt_synchronize(bdpt_ctx* ctx);
 
+/* ---- the reference's path tracer on the same substrate (src/integrators/path.h) ---- */
+typedef struct {
+    int32_t is_explicit;     /* [renderer] isExplicit (default true): renderExplicit / renderImplicit */
+    int32_t max_depth;       /* maxDepth (default -1 = Russian roulette past rr_depth) */
+    int32_t rr_depth;        /* rrDepth (default 5) */
+    float rr_prob;           /* rrProb (default 0.95) */
+    int32_t emitter_samples; /* emitterSamples (default 1) */
+    int32_t bsdf_samples;    /* bsdfSamples (default 0) */
+} bdpt_path_params;
+/* Renders every (pixel, sample) of the shard with PathTracerIntegrator::render
+ * and ADDS acc/spp per pixel to fb_device (same framebuffer, camera, seeding and
+ * shard conventions as bdpt_render; params->rr_depth / strategy are not used).
+ * Asynchronous. bdpt_get_stats().counters: [1] samples that outgrew the
+ * 512-level recursion stack (then the call's result is not the reference's;
+ * bdpt_render_path_host fails with BDPT_ERR_UNSUPPORTED), [2] / [3] samples
+ * that drew more than 227 / 624 random numbers; with BDPT_FLAG_COUNT also
+ * [0] closest-hit rays and [7] random numbers drawn. */
+int bdpt_render_path(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_path_params* path, float* fb_device,
+                     void* hip_stream);
+int bdpt_render_path_host(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_path_params* path,
+                          float* fb_host);
+
 /* ---- scene configuration and image output (host only, no GPU needed) ---- */
 
 /* The settings loadTOML (src/main.cpp:22-116) reads from a scene .toml, with its
@@ -162,6 +187,8 @@ typedef struct {
     int32_t rr_depth;        /* [renderer] rrDepth (bdpt/path, default 5) */
     float rr_prob;           /* [renderer] rrProb (bdpt default 0; unused: NO_RR, bdpt.h:18) */
     int32_t spp;             /* [renderer] spp (default 1) */
+    bdpt_path_params path;   /* type = "path": isExplicit, maxDepth, rrDepth, rrProb, emitterSamples,
+                                bsdfSamples (main.cpp:96-101); defaults otherwise */
 } bdpt_config;
 
 /* loadTOML (main.cpp:22-116). BDPT_ERR_INVALID with the parse error otherwise. */

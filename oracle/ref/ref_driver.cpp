@@ -334,6 +334,10 @@ int cmdToml(int argc, char** argv) {
            cfg.width, cfg.height, rt ? 1 : 0, (int)cfg.integrator);
     if (!rt && (cfg.integrator == EBDPTIntegrator || cfg.integrator == EPathTracerIntegrator))
         printf(", \"rrDepth\": %d, \"rrProb\": \"%a\"", cfg.integratorSettings.pt.rrDepth, cfg.integratorSettings.pt.rrProb);
+    if (!rt && cfg.integrator == EPathTracerIntegrator)
+        printf(", \"isExplicit\": %d, \"maxDepth\": %d, \"emitterSamples\": %zu, \"bsdfSamples\": %zu",
+               (int)cfg.integratorSettings.pt.isExplicit, cfg.integratorSettings.pt.maxDepth,
+               cfg.integratorSettings.pt.emitterSamples, cfg.integratorSettings.pt.bsdfSamples);
     if (!rt) printf(", \"spp\": %d", cfg.spp);
     printf("}\n");
     return 0;

@@ -67,6 +67,13 @@ def test_load_toml_matches_reference(path, expected):
     assert int(sc.realtime) == ref["realtime"]
     if not ref["realtime"]:
         assert INTEGRATORS[sc.integrator] == ref["integrator"]
+        if sc.integrator == "path":
+            assert (sc.path.rr_depth, c_hex(sc.path.rr_prob)) == (ref["rrDepth"], ref["rrProb"])
+            for k in ("isExplicit", "maxDepth", "emitterSamples", "bsdfSamples"):
+                if k in ref:
+                    got = {"isExplicit": int(sc.path.explicit), "maxDepth": sc.path.max_depth,
+                           "emitterSamples": sc.path.emitter_samples, "bsdfSamples": sc.path.bsdf_samples}[k]
+                    assert got == ref[k], k
         assert c.spp == ref["spp"]
         if "rrDepth" in ref:
             assert c.rr_depth == ref["rrDepth"]
@@ -165,9 +172,8 @@ def test_cli_without_gpu_rejects_non_bdpt_scenes(tmp_path):
     realtime passes are refused with the reference's error style."""
     cli = os.path.join(os.path.dirname(bdpt_amd.LIB_PATH), "tinyrender_amd")
     assert os.path.exists(cli)
-    r = subprocess.run([cli, os.path.join(GOLD, "config", "ref_bonus_cbox_bdpt_path.toml")], capture_output=True,
-                       text=True)
-    assert r.returncode != 0 and "not part of the MI355X BDPT path" in r.stderr
+    r = subprocess.run([cli, os.path.join(GOLD, "config", "t04_realtime.toml")], capture_output=True, text=True)
+    assert r.returncode != 0 and "realtime render passes are not part" in r.stderr
     r = subprocess.run([cli, os.path.join(GOLD, "config", "t05_bad_type.toml")], capture_output=True, text=True)
     assert r.returncode != 0 and "Error while parsing scene file" in r.stderr
     r = subprocess.run([cli], capture_output=True, text=True)
