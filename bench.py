@@ -59,7 +59,7 @@ def algorithmic_bytes_per_sample(c: dict, samples: int) -> float:
     return b / max(samples, 1)
 
 
-def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int) -> dict:
+def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int, integrator: str = "bdpt") -> dict:
     """The reference CPU path (oracle/_ref/ref_bdpt = the unmodified reference
     BDPT compiled from its sources) on a bounded sample of the same workload:
     every `stride`-th row of the 512x512 image at the bench spp, std::thread over
@@ -68,11 +68,13 @@ def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int) -> dict:
     ref = os.path.join(REPO, "oracle", "_ref", "ref_bdpt")
     toml = os.path.join("/tmp", f"bench_{scene}_{os.getpid()}.toml")
     with open(toml, "w") as f:
-        f.write(variants.toml_text(scene, W, H, spp, rr))
+        f.write(variants.toml_text(scene, W, H, spp, rr) if integrator == "bdpt"
+                else variants.path_toml_text(scene, W, H, spp))
     # ~6 rows per thread: 10-20 s of wall time at the reference's ~18 us per caustic sample-thread
     stride = max(1, H // (6 * threads))
     if os.path.exists(ref):
-        out = subprocess.run([ref, "render", toml, str(W), str(H), str(spp), "--rr", str(rr), "--threads",
+        rr_arg = ["--rr", str(rr)] if integrator == "bdpt" else []
+        out = subprocess.run([ref, "render", toml, str(W), str(H), str(spp), *rr_arg, "--threads",
                               str(threads), "--row-stride", str(stride)], capture_output=True, text=True,
                              check=True, timeout=900)
         r = json.loads(out.stdout.strip().splitlines()[-1])
@@ -80,7 +82,8 @@ def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int) -> dict:
     else:
         import oracle as O
         sc = O.Scene(variants.obj_path(scene))
-        p = O.make_params(variants.SCENES[scene]["camera"], W, H, spp, rr)
+        cam = variants.SCENES[scene]["camera"]
+        p = O.make_params(cam, W, H, spp, rr) if integrator == "bdpt" else O.make_path_params(cam, W, H, spp)
         t = time.time()
         _, samples = sc.render(p, threads=threads, rows=list(range(0, H, stride)))
         secs = time.time() - t
@@ -102,6 +105,9 @@ def main() -> None:
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--rr-depth", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--integrator", choices=["bdpt", "path"], default="bdpt",
+                    help="bdpt = the hot path (BASELINE metric); path = the reference's PathTracerIntegrator "
+                         "(path.h, cbox_bdpt_path.toml settings) on the same substrate, for comparison")
     ap.add_argument("--schedule", choices=["megakernel", "wavefront"], default="megakernel",
                     help="render schedule (BDPT_FLAG_WAVEFRONT for the shade/trace passes)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_caustic_512x512_256spp.json"),
@@ -122,8 +128,12 @@ def main() -> None:
     rr = args.rr_depth or sc["rr_depth"]
     W, H, spp = args.width, args.height, args.spp
     cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**sc["camera"]), width=W, height=H, spp=spp, rr_depth=rr)
-    integ = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
-                                    device=local if world > 1 else 0)
+    if args.integrator == "path":
+        integ = bdpt_amd.PathTracerIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
+                                              bdpt_amd.PathSettings(), device=local if world > 1 else 0)
+    else:
+        integ = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
+                                        device=local if world > 1 else 0)
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -160,7 +170,17 @@ def main() -> None:
     local_samples = integ.stats()["samples"]
     avg_kernel_ms = sum(kernel_ms) / max(len(kernel_ms), 1)
 
-    if rank == 0:
+    if rank == 0 and args.integrator == "path":
+        out = {"metric": "Msamples/sec, PathTracerIntegrator (path.h, explicit, RR 0.95 past depth 5)",
+               "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic camera samples",
+               "config": {"workload": f"path_{args.scene}_{W}x{H}_{spp}spp", "scene": SCENE_LABEL.get(args.scene),
+                          "kernel_ms": round(avg_kernel_ms, 3)}}
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(args.scene, W, H, spp, rr, integrator="path")
+        print(json.dumps(out), flush=True)
+    elif rank == 0:
         # algorithmic bytes per sample from a counting pass (untimed, same seeds, smaller spp)
         cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=min(spp, 16), rr_depth=rr)
         cnt = bdpt_amd.BDPTIntegrator(integ.scene, cnt_cfg, device=local if world > 1 else 0)
