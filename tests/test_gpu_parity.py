@@ -89,6 +89,8 @@ def test_gpu_full_traversal_equals_culled_traversal(sched):
     ("hardlight", 33, 17, 7, 3),
     ("hardlight_mirror", 32, 32, 2, 9),
     ("cbox_low", 17, 29, 1, 6),
+    ("cbox_low", 16, 12, 4, 28),  # the deepest rrDepth the lazy MT19937 window covers (226 draws)
+    ("synth1m", 12, 8, 2, 8),     # 1M triangles, 4-wide stack spills past the LDS entries
 ])
 def test_gpu_matches_oracle_other_configs(name, W, H, spp, rr):
     it = integrator(name, W, H, spp, rr)
@@ -98,6 +100,13 @@ def test_gpu_matches_oracle_other_configs(name, W, H, spp, rr):
     assert n == W * H * spp
     worst, exact, _ = report(fb, ref)
     assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
+
+
+def test_gpu_rr_depth_beyond_lazy_window_is_refused():
+    """rrDepth 29 can need 234 draws > 227: an error, never a wrong image."""
+    it = integrator("cbox_low", 8, 8, 1, 29)
+    with pytest.raises(bdpt_amd.BdptError, match="rr_depth"):
+        it.render_frame()
 
 
 def test_gpu_camera_facing_away_renders_black():
