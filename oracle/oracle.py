@@ -35,7 +35,23 @@ class Params(ctypes.Structure):
         ("pt_rr_prob", ctypes.c_float),
         ("pt_emitter_samples", ctypes.c_int),
         ("pt_bsdf_samples", ctypes.c_int),
+        ("di_strategy", ctypes.c_int),  # DirectIntegrator samplingStrategy (DIRECT_STRATEGIES)
+        ("di_emitter_samples", ctypes.c_int),
+        ("di_bsdf_samples", ctypes.c_int),
     ]
+
+
+DIRECT_STRATEGIES = {"area": 1, "solidAngle": 2, "cosineHemisphere": 3, "bsdf": 4, "mis": 5}
+
+
+def make_direct_params(cam: dict, width: int, height: int, spp: int, strategy: str = "mis", emitter_samples: int = 1,
+                       bsdf_samples: int = 1) -> "Params":
+    """Params for DirectIntegrator (direct.h); defaults of main.cpp:90-92 except the strategy."""
+    p = make_params(cam, width, height, spp, 1)
+    p.integrator = 2
+    p.di_strategy = DIRECT_STRATEGIES[strategy]
+    p.di_emitter_samples, p.di_bsdf_samples = emitter_samples, bsdf_samples
+    return p
 
 
 # [renderer] defaults of a type = "path" scene (main.cpp:96-101)

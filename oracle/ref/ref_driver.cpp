@@ -28,6 +28,14 @@
 
 #include <integrators/bdpt.h>
 #include <integrators/path.h>
+// direct.h defines two non-inline free functions that renderer.cpp (which
+// includes it for its factory) also defines: renamed here so the driver can
+// instantiate DirectIntegrator without a duplicate symbol. Same code.
+#define quadratic tr_driver_quadratic
+#define raySphereIntersect tr_driver_raySphereIntersect
+#include <integrators/direct.h>
+#undef quadratic
+#undef raySphereIntersect
 #include <bsdfs/mixture.h>
 #include <bsdfs/glass.h>
 
@@ -110,6 +118,7 @@ void setup(Setup& s, const std::string& toml, int W, int H, int spp, int rr) {
     // the offline integrator the TOML names: "bdpt" (the hot path) or "path"
     // (PathTracerIntegrator, src/integrators/path.h, with its TOML settings)
     if (s.cfg.integrator == EPathTracerIntegrator) s.integ.reset(new PathTracerIntegrator(*s.scene));
+    else if (s.cfg.integrator == EDirectIntegrator) s.integ.reset(new DirectIntegrator(*s.scene));
     else s.integ.reset(new BDPTIntegrator(*s.scene));
     s.rrDepth = s.cfg.integratorSettings.pt.rrDepth;
     s.integ->init();
@@ -338,6 +347,10 @@ int cmdToml(int argc, char** argv) {
         printf(", \"isExplicit\": %d, \"maxDepth\": %d, \"emitterSamples\": %zu, \"bsdfSamples\": %zu",
                (int)cfg.integratorSettings.pt.isExplicit, cfg.integratorSettings.pt.maxDepth,
                cfg.integratorSettings.pt.emitterSamples, cfg.integratorSettings.pt.bsdfSamples);
+    if (!rt && cfg.integrator == EDirectIntegrator)
+        printf(", \"emitterSamples\": %zu, \"bsdfSamples\": %zu, \"samplingStrategy\": \"%s\"",
+               cfg.integratorSettings.di.emitterSamples, cfg.integratorSettings.di.bsdfSamples,
+               cfg.integratorSettings.di.samplingStrategy.c_str());
     if (!rt) printf(", \"spp\": %d", cfg.spp);
     printf("}\n");
     return 0;

@@ -34,6 +34,9 @@ typedef struct {
     int pt_explicit, pt_max_depth, pt_rr_depth;
     float pt_rr_prob;
     int pt_emitter_samples, pt_bsdf_samples;
+    /* integrator 2: DirectIntegrator (direct.h), samplingStrategy 1 area, 2 solidAngle,
+     * 3 cosineHemisphere, 4 bsdf, 5 mis (main.cpp:88-92) */
+    int di_strategy, di_emitter_samples, di_bsdf_samples;
 } tro_params;
 
 /* Loads an OBJ (+ MTL) exactly as Scene::load does (reference

@@ -936,7 +936,180 @@ static v3 pt_render(const ctx_t* c, ray_t ray, tr_sampler* smp) {
     return c->p->pt_explicit ? pt_explicit(c, smp, &hit, 0) : pt_implicit(c, smp, &hit, 0);
 }
 
+/* -------------------------------------------------------- direct lighting */
+/* DirectIntegrator (src/integrators/direct.h): emitters are treated as spheres
+ * of their shape's corner mean and AABB half-width (renderer.cpp:349-358). */
+
+/* quadratic + raySphereIntersect (direct.h:17-67), in double as there. */
+static int ray_sphere_hit(const ray_t* r, v3 center, float radius) {
+    v3 no = vsub(r->o, center);
+    double cc = (double)(vdot(no, no) - (radius * radius));
+    double b = (double)vdot(no, r->d) * 2.0;
+    double a = (double)vdot(r->d, r->d);
+    double disc = b * b - 4 * a * cc;
+    double t0, t1;
+    if (disc > 0) {
+        double sq = sqrt(disc);
+        double inv2a = 1 / (2 * a);
+        t0 = (-b + sq) * inv2a;
+        t1 = (-b - sq) * inv2a;
+    } else if (disc == 0) {
+        t0 = (-b + sqrt(disc)) / (2 * a);
+        t1 = t0;
+    } else {
+        return 0;
+    }
+    const double lo = r->min_t, hi = r->max_t;
+    return (t0 > lo && t0 < hi) || (t1 > lo && t1 < hi);
+}
+/* Warp::squareToUniformSphere (math.h:119-127) */
+static v3 sq_uniform_sphere(v2 u) {
+    float phi = u.x * TR_PI * 2.0f;
+    float cosTheta = 1.f - (2.f * u.y);
+    float sinTheta = tr_sqrtf(fmaxf(1.f - cosTheta * cosTheta, 0.f));
+    return V3(sinTheta * tr_cosf(phi), sinTheta * tr_sinf(phi), cosTheta);
+}
+/* sampleSphereBySolidAngle (direct.h:109-141) */
+static v3 sample_sphere_solid_angle(v2 u, v3 p, v3 center, float radius, float* pdf) {
+    v3 cdir = vnormalize(vsub(center, p));
+    frame_t f = make_frame(cdir);
+    v3 dd = vsub(center, p);
+    float sin2 = radius * radius / vdot(dd, dd);
+    float cosMax = tr_sqrtf(fmaxf(0.f, 1.f - sin2));
+    float cosTheta = (1.f - u.x) + (u.x * cosMax);
+    float phi = u.y * TR_PI * 2.0f;
+    float sinTheta = tr_sqrtf(fmaxf(1.f - (cosTheta * cosTheta), 0.f));
+    v3 d = V3(sinTheta * tr_cosf(phi), sinTheta * tr_sinf(phi), cosTheta);
+    *pdf = TR_INV_TWOPI * (1.f / (1.f - cosMax));
+    return to_world(&f, d);
+}
+
+static v3 di_render(const ctx_t* c, ray_t ray, tr_sampler* smp) {
+    const tro_scene* s = c->s;
+    const tro_params* P = c->p;
+    const int es = P->di_emitter_samples, bs = P->di_bsdf_samples, strat = P->di_strategy;
+    v3 Lr = V3(0, 0, 0);
+    hit_t hit = zero_hit();
+    if (!scene_intersect(s, &ray, &hit)) return Lr;
+    v3 le = emission_of(s, &hit);
+    if (!veq0(le)) return le;
+    const tro_bsdf* b = bsdf_of(s, &hit);
+    if (strat == 1 || strat == 2) { /* renderArea (:143-195) / renderSolidAngle (:244-311) */
+        for (int i = 0; i < es; ++i) {
+            float emitterPdf;
+            int id = select_emitter(s, s_next(smp), &emitterPdf);
+            const tro_emitter* e = &s->emit[id];
+            v2 u = s_next2d(smp);
+            if (strat == 1) {
+                v3 ne = sq_uniform_sphere(u);
+                v3 pos = vadd(vscale(ne, e->radius), e->center);
+                v3 wiW = vnormalize(vsub(pos, hit.p));
+                float pdf = 1.f / (4 * TR_PI * e->radius * e->radius);
+                v3 dd = vsub(hit.p, pos);
+                float d2 = vdot(dd, dd);
+                float cosOut = vdot(vneg(wiW), ne);
+                v3 wil = to_local(&hit.fs, wiW);
+                if (cosOut <= 0.f || wil.z <= 0.f) continue;
+                ray_t r = {hit.p, wiW, TR_EPSILON, tr_sqrtf(d2) - TR_EPSILON};
+                hit_t vis = zero_hit();
+                if (!scene_intersect(s, &r, &vis)) {
+                    hit.wi = wil;
+                    float a2s = cosOut * (1.f / d2);
+                    v3 t = vmul(e->radiance, bsdf_eval(b, &hit));
+                    Lr = vadd(Lr, vscale(vscale(vscale(t, 1.f / pdf), 1.f / emitterPdf), a2s));
+                }
+            } else {
+                float pdf;
+                v3 wiW = sample_sphere_solid_angle(u, hit.p, e->center, e->radius, &pdf);
+                v3 wil = to_local(&hit.fs, wiW);
+                if (wil.z <= 0.f) continue;
+                v3 dc = vsub(e->center, hit.p);
+                ray_t r = {hit.p, wiW, TR_EPSILON, tr_sqrtf(vdot(dc, dc)) + TR_EPSILON}; /* glm::distance */
+                hit_t vis = zero_hit();
+                int vh = scene_intersect(s, &r, &vis);
+                if ((vh && vis.shape == e->shape) || (!vh && ray_sphere_hit(&r, e->center, e->radius))) {
+                    hit.wi = wil;
+                    v3 t = vmul(e->radiance, bsdf_eval(b, &hit));
+                    Lr = vadd(Lr, vscale(vscale(t, 1.f / pdf), 1.f / emitterPdf));
+                }
+            }
+        }
+        return vdivs(Lr, (float)es);
+    }
+    if (strat == 3) { /* renderCosineHemisphere (:198-233) */
+        for (int i = 0; i < es; ++i) {
+            v3 local = sq_cosine_hemisphere(s_next2d(smp));
+            v3 world = vnormalize(to_world(&hit.fs, local));
+            ray_t r = {hit.p, world, TR_EPSILON, INFINITY};
+            hit_t vis = zero_hit();
+            if (scene_intersect(s, &r, &vis)) {
+                hit.wi = local;
+                v3 t = vmul(emission_of(s, &vis), bsdf_eval(b, &hit));
+                Lr = vadd(Lr, vscale(t, 1.0f / cosine_pdf(local)));
+            }
+        }
+        return vdivs(Lr, (float)es);
+    }
+    if (strat == 4) { /* renderBSDF (:235-264) */
+        for (int i = 0; i < bs; ++i) {
+            float pdf;
+            v3 f = bsdf_sample(b, &hit, s_next2d(smp), &pdf);
+            ray_t r = {hit.p, to_world(&hit.fs, hit.wi), TR_EPSILON, INFINITY};
+            hit_t vis = zero_hit();
+            if (scene_intersect(s, &r, &vis))
+                Lr = vadd(Lr, vscale(vmul(emission_of(s, &vis), f), (float)(1.0 / (double)pdf)));
+        }
+        return vdivs(Lr, (float)bs);
+    }
+    if (strat != 5) abort(); /* "Error: wrong strategy" (direct.h:440-441) */
+    /* renderMIS (:313-428) */
+    v3 eEst = V3(0, 0, 0), bEst = V3(0, 0, 0);
+    for (int i = 0; i < es; ++i) {
+        float emitterPdf;
+        int id = select_emitter(s, s_next(smp), &emitterPdf);
+        const tro_emitter* e = &s->emit[id];
+        v2 u = s_next2d(smp);
+        float pdf;
+        v3 wiW = sample_sphere_solid_angle(u, hit.p, e->center, e->radius, &pdf);
+        v3 wil = to_local(&hit.fs, wiW);
+        if (wil.z <= 0.f) continue;
+        ray_t r = {hit.p, wiW, TR_EPSILON, INFINITY};
+        hit_t vis = zero_hit();
+        int vh = scene_intersect(s, &r, &vis);
+        if ((vh && vis.shape == e->shape) || (!vh && ray_sphere_hit(&r, e->center, e->radius))) {
+            hit.wi = wil;
+            float bsdfPdf = bsdf_pdf(b, &hit);
+            float w = balance_heuristic((float)es, pdf * emitterPdf, (float)bs, bsdfPdf);
+            v3 t = vscale(vmul(e->radiance, bsdf_eval(b, &hit)), w);
+            eEst = vadd(eEst, vscale(vscale(t, 1.f / pdf), 1.f / emitterPdf));
+        }
+    }
+    eEst = es == 0 ? V3(0, 0, 0) : vdivs(eEst, (float)es);
+    for (int i = 0; i < bs; ++i) {
+        float pdf;
+        v3 f = bsdf_sample(b, &hit, s_next2d(smp), &pdf);
+        ray_t r = {hit.p, to_world(&hit.fs, hit.wi), TR_EPSILON, INFINITY};
+        hit_t vis = zero_hit();
+        if (!scene_intersect(s, &r, &vis)) continue;
+        v3 Le = emission_of(s, &vis);
+        if (veq0(Le)) continue;
+        int eid = s->shape_emitter[vis.shape];
+        if (eid < 0) abort(); /* the reference asserts */
+        const tro_emitter* e = &s->emit[eid];
+        v3 dd = vsub(hit.p, e->center);
+        float sin2 = e->radius * e->radius / vdot(dd, dd);
+        float cosMax = tr_sqrtf(fmaxf(0.f, 1.f - sin2));
+        float esap = TR_INV_TWOPI * (1.f / (1.f - cosMax));
+        esap *= 1.f / (float)s->nemit;
+        float w = balance_heuristic((float)bs, pdf, (float)es, esap);
+        bEst = vadd(bEst, vscale(vscale(vmul(Le, f), w), 1.f / pdf));
+    }
+    bEst = bs == 0 ? V3(0, 0, 0) : vdivs(bEst, (float)bs);
+    return vadd(Lr, vadd(eEst, bEst));
+}
+
 static v3 integrator_render(const ctx_t* c, ray_t ray, tr_sampler* smp) {
+    if (c->p->integrator == 2) return di_render(c, ray, smp);
     return c->p->integrator == 1 ? pt_render(c, ray, smp) : bdpt_render(c, ray, smp);
 }
 

@@ -48,6 +48,8 @@ typedef struct {
     v3 radiance;
     int ncdf;
     float* cdf; /* ncdf = faces + 1 */
+    v3 center;    /* worldData.shapesCenter (renderer.cpp:295-304): mean of the shape's corners */
+    float radius; /* Scene::getShapeRadius (renderer.cpp:349-353): AABB max.x - center.x */
 } tro_emitter;
 
 typedef struct {

@@ -772,6 +772,18 @@ tro_scene* tro_scene_load(const char* obj_path) {
                 e->cdf[f + 1] = e->cdf[f] + 0.5f * sqrtf((e3.x * e3.x + e3.y * e3.y) + e3.z * e3.z);
             }
             e->area = e->cdf[e->ncdf - 1];
+            /* shape center and "radius" as the direct integrator reads them (renderer.cpp:295-304, :349-358) */
+            v3 c = V3(0.f, 0.f, 0.f);
+            float maxx = -INFINITY;
+            for (int f = 0; f < s->shape_count[sh]; f++) {
+                const float* p = s->tv + 9 * (size_t)(s->shape_first[sh] + f);
+                for (int k = 0; k < 3; k++) {
+                    c = vadd(c, V3(p[3 * k], p[3 * k + 1], p[3 * k + 2]));
+                    maxx = (maxx < p[3 * k]) ? p[3 * k] : maxx; /* std::max */
+                }
+            }
+            e->center = vdivs(c, (float)(3 * s->shape_count[sh]));
+            e->radius = maxx - e->center.x;
             float sum = e->cdf[e->ncdf - 1];
             for (int f = 0; f < e->ncdf; f++) e->cdf[f] /= sum;
             s->shape_emitter[sh] = s->nemit;

@@ -61,6 +61,21 @@ PATH_FRAMEBUFFERS = {
     "P5_hardlight_path_maxdepth3_48x48_spp4": ("hardlight", 48, 48, 4, dict(max_depth=3, bsdf_samples=1)),
 }
 
+# DirectIntegrator (src/integrators/direct.h) frames: name: (scene, W, H, spp, direct settings). Its
+# emitters are treated as spheres (shape center, AABB half-width, renderer.cpp:349-358).
+DIRECT_FRAMEBUFFERS = {
+    "D1_caustic_direct_area_48x48_spp4": ("caustic", 48, 48, 4, dict(strategy="area", emitter_samples=2)),
+    "D2_hardlight_direct_solidangle_48x48_spp4": ("hardlight", 48, 48, 4, dict(strategy="solidAngle",
+                                                                                emitter_samples=2)),
+    "D3_caustic_direct_cosine_48x48_spp4": ("caustic", 48, 48, 4, dict(strategy="cosineHemisphere",
+                                                                        emitter_samples=3)),
+    "D4_hardlight_direct_bsdf_48x48_spp4": ("hardlight", 48, 48, 4, dict(strategy="bsdf", bsdf_samples=3)),
+    "D5_caustic_direct_mis_48x48_spp4": ("caustic", 48, 48, 4, dict(strategy="mis", emitter_samples=2,
+                                                                     bsdf_samples=2)),
+    "D6_hardlight_direct_mis_48x48_spp4": ("hardlight", 48, 48, 4, dict(strategy="mis", emitter_samples=1,
+                                                                         bsdf_samples=1)),
+}
+
 SCENE_DUMPS = {"cbox_low": (64, 64), "caustic": (512, 512), "hardlight": (512, 512), "hardlight_mirror": (512, 512),
                "synth1m": (64, 64)}
 
@@ -87,6 +102,9 @@ def main() -> None:
         "framebuffers": dict(old.get("framebuffers", {})),
         "scenes": dict(old.get("scenes", {})),
     }
+    for sect in ("path_framebuffers", "direct_framebuffers"):
+        if sect in old:
+            manifest[sect] = dict(old[sect])
     tmp = tempfile.mkdtemp()
     for name, entry in FRAMEBUFFERS.items():
         if only and name not in only:
@@ -128,6 +146,24 @@ def main() -> None:
                                                    mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
                                                    ref_seconds=info["seconds"])
         print(name, manifest["path_framebuffers"][name]["sha256"][:16], info)
+    for name, (scene, W, H, spp, direct) in DIRECT_FRAMEBUFFERS.items():
+        if only and name not in only:
+            continue
+        toml = os.path.join(tmp, name + ".toml")
+        with open(toml, "w") as f:
+            f.write(variants.direct_toml_text(scene, W, H, spp, **direct))
+        out = os.path.join(tmp, name + ".f32")
+        r = subprocess.run([REF, "render", toml, str(W), str(H), str(spp), "--out", out], capture_output=True,
+                           text=True, check=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        fb = np.fromfile(out, np.float32)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), fb=fb)
+        manifest.setdefault("direct_framebuffers", dict(old.get("direct_framebuffers", {})))
+        manifest["direct_framebuffers"][name] = dict(scene=scene, width=W, height=H, spp=spp, direct=direct,
+                                                     samples=info["samples"], sha256=sha(fb.tobytes()),
+                                                     mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
+                                                     ref_seconds=info["seconds"])
+        print(name, manifest["direct_framebuffers"][name]["sha256"][:16], info)
     for scene, (W, H) in SCENE_DUMPS.items():
         if only and scene not in only:
             continue

@@ -128,3 +128,22 @@ def test_oracle_path_tracer_bit_exact(name, golden_manifest):
     assert hashlib.sha256(ref.tobytes()).hexdigest() == meta["sha256"]
     mism = np.flatnonzero(fb.view(np.uint32) != ref.view(np.uint32))
     assert mism.size == 0, f"{mism.size} floats differ, first at {mism[:5]}"
+
+
+DIRECT_CASES = ["D1_caustic_direct_area_48x48_spp4", "D2_hardlight_direct_solidangle_48x48_spp4",
+                "D3_caustic_direct_cosine_48x48_spp4", "D4_hardlight_direct_bsdf_48x48_spp4",
+                "D5_caustic_direct_mis_48x48_spp4", "D6_hardlight_direct_mis_48x48_spp4"]
+
+
+@pytest.mark.parametrize("name", DIRECT_CASES)
+def test_oracle_direct_integrator_bit_exact(name, golden_manifest):
+    """DirectIntegrator (direct.h), every sampling strategy, frames rendered by the reference."""
+    meta = golden_manifest["direct_framebuffers"][name]
+    sc = variants.SCENES[meta["scene"]]
+    p = O.make_direct_params(sc["camera"], meta["width"], meta["height"], meta["spp"], **meta["direct"])
+    fb, n = O.Scene(variants.obj_path(meta["scene"])).render(p)
+    assert n == meta["samples"]
+    ref = load_golden(name)
+    assert hashlib.sha256(ref.tobytes()).hexdigest() == meta["sha256"]
+    mism = np.flatnonzero(fb.view(np.uint32) != ref.view(np.uint32))
+    assert mism.size == 0, f"{mism.size} floats differ, first at {mism[:5]}"
