@@ -70,12 +70,17 @@ class _PathParams(ctypes.Structure):  # bdpt_path_params
                 ("rr_prob", ctypes.c_float), ("emitter_samples", ctypes.c_int32), ("bsdf_samples", ctypes.c_int32)]
 
 
+class _DirectParams(ctypes.Structure):  # bdpt_direct_params
+    _fields_ = [("sampling_strategy", ctypes.c_int32), ("emitter_samples", ctypes.c_int32),
+                ("bsdf_samples", ctypes.c_int32)]
+
+
 class _Config(ctypes.Structure):  # bdpt_config
     _fields_ = [("toml_file", ctypes.c_char * 4096), ("obj_file_raw", ctypes.c_char * 4096),
                 ("obj_file", ctypes.c_char * 4096), ("camera", _Camera), ("width", ctypes.c_int32),
                 ("height", ctypes.c_int32), ("realtime", ctypes.c_int32), ("integrator", ctypes.c_char * 32),
                 ("rr_depth", ctypes.c_int32), ("rr_prob", ctypes.c_float), ("spp", ctypes.c_int32),
-                ("path", _PathParams)]
+                ("path", _PathParams), ("direct", _DirectParams), ("sampling_strategy", ctypes.c_char * 32)]
 
 
 class _Stats(ctypes.Structure):
@@ -119,6 +124,10 @@ def lib():
         L.bdpt_config_load_toml.argtypes = [ctypes.c_char_p, ctypes.POINTER(_Config)]
         L.bdpt_render_path.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_PathParams), vp, vp]
         L.bdpt_render_path_host.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_PathParams), vp]
+        L.bdpt_render_direct.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_DirectParams), vp, vp]
+        L.bdpt_render_direct_host.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_DirectParams), vp]
+        L.bdpt_direct_strategy.restype = i32
+        L.bdpt_direct_strategy.argtypes = [ctypes.c_char_p]
         L.bdpt_encode_exr.argtypes = [vp, i32, i32, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         L.bdpt_save_exr.argtypes = [vp, i32, i32, ctypes.c_char_p]
         _lib = L
@@ -180,6 +189,24 @@ class PathSettings:
         return p
 
 
+# DirectIntegrator::render's samplingStrategy strings (direct.h:450-461) -> BDPT_DIRECT_*
+DIRECT_STRATEGIES = {"area": 1, "solidAngle": 2, "cosineHemisphere": 3, "bsdf": 4, "mis": 5}
+
+
+@dataclass
+class DirectSettings:
+    """DirectIntegrator settings ([renderer] of a type = "direct" scene, main.cpp:88-92)."""
+    sampling_strategy: str = "emitter"  # the reference's default, which its render() rejects
+    emitter_samples: int = 1
+    bsdf_samples: int = 1
+
+    def c(self) -> _DirectParams:
+        d = _DirectParams()
+        d.sampling_strategy = DIRECT_STRATEGIES.get(self.sampling_strategy, 0)
+        d.emitter_samples, d.bsdf_samples = self.emitter_samples, self.bsdf_samples
+        return d
+
+
 @dataclass
 class SceneConfig:
     """loadTOML's result (main.cpp:22-116): the scene file settings, plus the
@@ -191,6 +218,7 @@ class SceneConfig:
     realtime: bool
     integrator: str
     path: PathSettings = field(default_factory=PathSettings)
+    direct: DirectSettings = field(default_factory=DirectSettings)
 
 
 def load_toml(path: str) -> SceneConfig:
@@ -201,9 +229,11 @@ def load_toml(path: str) -> SceneConfig:
     pp = c.path
     path = PathSettings(explicit=bool(pp.is_explicit), max_depth=pp.max_depth, rr_depth=pp.rr_depth,
                         rr_prob=pp.rr_prob, emitter_samples=pp.emitter_samples, bsdf_samples=pp.bsdf_samples)
+    direct = DirectSettings(sampling_strategy=c.sampling_strategy.decode(), emitter_samples=c.direct.emitter_samples,
+                            bsdf_samples=c.direct.bsdf_samples)
     return SceneConfig(toml_file=c.toml_file.decode(), obj_file=c.obj_file.decode(),
                        obj_file_raw=c.obj_file_raw.decode(), config=cfg, realtime=bool(c.realtime),
-                       integrator=c.integrator.decode(), path=path)
+                       integrator=c.integrator.decode(), path=path, direct=direct)
 
 
 def encode_exr(rgb: np.ndarray, width: int, height: int) -> bytes:
@@ -380,3 +410,30 @@ class PathTracerIntegrator(BDPTIntegrator):
         p, pp = self.params(row_offset, row_stride, flags), self.path.c()
         _check(lib().bdpt_render_path(self._h, ctypes.byref(p), ctypes.byref(pp), ctypes.c_void_p(fb_ptr),
                                       ctypes.c_void_p(stream_ptr)))
+
+
+class DirectIntegrator(BDPTIntegrator):
+    """The reference's DirectIntegrator (src/integrators/direct.h) on the same GPU
+    substrate: one bounce of direct light by area, solid-angle, cosine-hemisphere,
+    BSDF or MIS sampling, with the emitters as the spheres the reference makes of
+    them (renderer.cpp:349-358)."""
+
+    def __init__(self, scene: Scene, config: Config, direct: DirectSettings | None = None, device: int = 0):
+        super().__init__(scene, config, device)
+        self.direct = direct or DirectSettings(sampling_strategy="mis")
+
+    def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:  # noqa: D102
+        raise BdptError("single-sample render(ray, sampler) is only exported for the BDPT integrator")
+
+    def render_frame(self, row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> np.ndarray:
+        if self.rgb is None:
+            self.init()
+        p, d = self.params(row_offset, row_stride, flags), self.direct.c()
+        _check(lib().bdpt_render_direct_host(self._h, ctypes.byref(p), ctypes.byref(d), self.rgb.ctypes.data))
+        return self.rgb
+
+    def render_device(self, fb_ptr: int, stream_ptr: int = 0, row_offset: int = 0, row_stride: int = 1,
+                      flags: int = 0) -> None:
+        p, d = self.params(row_offset, row_stride, flags), self.direct.c()
+        _check(lib().bdpt_render_direct(self._h, ctypes.byref(p), ctypes.byref(d), ctypes.c_void_p(fb_ptr),
+                                        ctypes.c_void_p(stream_ptr)))

@@ -40,7 +40,7 @@ int wf_parts();
 int frame_kernel_blocks_per_cu(size_t dyn_lds);
 size_t pt_params_bytes();
 int pt_blocks_per_cu(size_t dyn_lds);
-hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[7], float* fb,
+hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8], float* fb,
                      float4* levels, uint32_t* ring, uint2* gstack, uint32_t nslots, unsigned long long* work,
                      unsigned long long* counters, int grid, hipStream_t stream, void* dparams);
 int frame_kernel_block();
@@ -516,8 +516,8 @@ int bdpt_render_path(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_pa
     if ((rc = ensure_pt(c, levels))) return rc;
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const dev::DevFrame fr = make_frame(p);
-    int32_t settings[7] = {path->is_explicit ? 1 : 0, path->max_depth, path->rr_depth, 0, path->emitter_samples,
-                           path->bsdf_samples, levels};
+    int32_t settings[8] = {path->is_explicit ? 1 : 0, path->max_depth, path->rr_depth, 0, path->emitter_samples,
+                           path->bsdf_samples, levels, 0};
     std::memcpy(&settings[3], &path->rr_prob, 4);
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
@@ -548,6 +548,52 @@ int bdpt_render_path_host(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_pa
     if ((rc = bdpt_get_stats(c, &st))) return rc;
     if (st.counters[1] != 0)
         return fail(BDPT_ERR_UNSUPPORTED, std::to_string(st.counters[1]) + " samples outgrew the path tracer's level stack");
+    return BDPT_OK;
+}
+
+// DirectIntegrator (direct.h) on the path tracer's kernel: one level, no recursion.
+int bdpt_render_direct(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direct_params* d, float* fb,
+                       void* hip_stream) {
+    if (!c || !fb || !d) return fail(BDPT_ERR_INVALID, "null argument");
+    if (!p) return fail(BDPT_ERR_INVALID, "null params");
+    if (p->width <= 0 || p->height <= 0 || p->spp <= 0) return fail(BDPT_ERR_INVALID, "width/height/spp must be > 0");
+    if (static_cast<int64_t>(p->width) * p->height >= (1ll << 31))
+        return fail(BDPT_ERR_INVALID, "image too large (W*H must fit int32, as in the reference)");
+    if (p->row_stride < 1 || p->row_offset < 0) return fail(BDPT_ERR_INVALID, "bad row shard");
+    if (d->sampling_strategy < BDPT_DIRECT_AREA || d->sampling_strategy > BDPT_DIRECT_MIS)
+        return fail(BDPT_ERR_INVALID, "Error: wrong strategy");  // direct.h:460
+    if (d->emitter_samples < 0 || d->bsdf_samples < 0) return fail(BDPT_ERR_INVALID, "negative sample counts");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = ensure_pt(c, 1))) return rc;
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    const dev::DevFrame fr = make_frame(p);
+    const int32_t settings[8] = {1, -1, 0, 0, d->emitter_samples, d->bsdf_samples, 1, d->sampling_strategy};
+    HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
+    HIP_TRY(hipEventRecord(c->ev0, st));
+    if (fr.total_samples > 0)
+        HIP_TRY(launch_pt(c->sc, fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
+                          c->counters, c->pt_grid, st, c->pt_dparams));
+    HIP_TRY(hipEventRecord(c->ev1, st));
+    c->pending_timing = true;
+    c->stats = bdpt_stats{};
+    c->stats.samples = static_cast<int64_t>(fr.total_samples);
+    c->stats.launches = fr.total_samples > 0 ? 1 : 0;
+    return BDPT_OK;
+}
+
+int bdpt_render_direct_host(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direct_params* d, float* fb_host) {
+    if (!c || !fb_host || !p) return fail(BDPT_ERR_INVALID, "null argument");
+    if (p->width <= 0 || p->height <= 0) return fail(BDPT_ERR_INVALID, "width/height must be > 0");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = static_cast<size_t>(p->width) * p->height * 3;
+    int rc;
+    if ((rc = ensure_tmp_fb(c, n))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->tmp_fb, fb_host, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if ((rc = bdpt_render_direct(c, p, d, c->tmp_fb, c->stream))) return rc;
+    HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return BDPT_OK;
 }
 

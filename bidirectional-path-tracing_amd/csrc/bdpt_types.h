@@ -50,6 +50,10 @@ struct EmitterRecord {
     int32_t cdf_offset;   // into emit_cdf (nfaces + 1 entries)
     float area;
     float radiance[3];
+    // The emitter as a sphere, for DirectIntegrator (direct.h): the shape's corner
+    // mean (renderer.cpp:295-304) and AABB max.x - center.x (renderer.cpp:349-353).
+    float center[3];
+    float radius;
 };
 
 struct CameraConstants {

@@ -93,7 +93,10 @@ struct PtSettings {
     float rr_prob;
     int32_t emitter_samples, bsdf_samples;
     int32_t max_levels;  // capacity of the level stack
+    int32_t direct;      // 1..5: DirectIntegrator with samplingStrategy area, solidAngle,
+                         // cosineHemisphere, bsdf, mis (direct.h:430-442); 0: the path tracer
 };
+enum : int32_t { DI_AREA = 1, DI_SOLID_ANGLE = 2, DI_COSINE = 3, DI_BSDF = 4, DI_MIS = 5 };
 
 struct PtParams {
     DevScene sc;
@@ -116,6 +119,8 @@ enum : uint32_t {  // the query a lane waits on / the step it resumes at
     PQ_DIRE,     // explicit direct light, emitter sample (path.h:134)
     PQ_DIRB,     // explicit direct light, BSDF sample (path.h:162)
     PQ_IMP,      // implicit (path.h:43)
+    PQ_DI_E,     // direct integrator, emitter / cosine sample (direct.h:177, :216, :275, :345)
+    PQ_DI_B,     // direct integrator, BSDF sample (direct.h:249, :387)
 };
 
 struct PtLane {
@@ -135,6 +140,7 @@ struct PtLane {
     float e_cos, e_d2, e_pdf, e_apdf;
     f3 e_wil, b_f, wiw;
     float b_pdf;
+    int e_id;                   // direct integrator: the sampled emitter
 };
 
 __device__ __forceinline__ f3 emission_of(const DevScene& sc, int mat) { return ld3(bsdf_of(sc, mat).emission); }
@@ -185,6 +191,51 @@ __device__ __forceinline__ void pt_finish(PtLane& L, const PtParams& P, f3 Li) {
     L.q = PQ_NONE;
 }
 
+// quadratic + raySphereIntersect (direct.h:17-67) in double, as there: true
+// when a root lies strictly inside (min_t, max_t).
+__device__ BDPT_NOINLINE bool ray_sphere_hit(Ray r, f3 center, float radius) {
+    const f3 no = r.o - center;
+    const double cc = static_cast<double>(dot(no, no) - (radius * radius));
+    const double b = static_cast<double>(dot(no, r.d)) * 2.0;
+    const double a = static_cast<double>(dot(r.d, r.d));
+    const double disc = b * b - 4 * a * cc;
+    double t0, t1;
+    if (disc > 0) {
+        const double sq = __builtin_sqrt(disc);
+        const double inv2a = 1 / (2 * a);
+        t0 = (-b + sq) * inv2a;
+        t1 = (-b - sq) * inv2a;
+    } else if (disc == 0) {
+        t0 = (-b + __builtin_sqrt(disc)) / (2 * a);
+        t1 = t0;
+    } else {
+        return false;
+    }
+    const double lo = r.min_t, hi = r.max_t;
+    return (t0 > lo && t0 < hi) || (t1 > lo && t1 < hi);
+}
+// Warp::squareToUniformSphere (math.h:119-127)
+__device__ __forceinline__ f3 uniform_sphere(F2 u) {
+    const float phi = u.x * kPi * 2.0f;
+    const float cosTheta = 1.f - (2.f * u.y);
+    const float sinTheta = sqrt_cr(glibc_fmaxf(1.f - cosTheta * cosTheta, 0.f));
+    const SinCos sc = glibc_sincosf2(phi);
+    return mk(sinTheta * sc.c, sinTheta * sc.s, cosTheta);
+}
+// sampleSphereBySolidAngle (direct.h:109-141)
+__device__ __forceinline__ f3 sphere_solid_angle(F2 u, f3 p, f3 center, float radius, float& pdf) {
+    const f3 cdir = normalize(center - p);
+    const f3 dd = center - p;
+    const float sin2 = radius * radius / dot(dd, dd);
+    const float cosMax = sqrt_cr(glibc_fmaxf(0.f, 1.f - sin2));
+    const float cosTheta = (1.f - u.x) + (u.x * cosMax);
+    const float phi = u.y * kPi * 2.0f;
+    const float sinTheta = sqrt_cr(glibc_fmaxf(1.f - (cosTheta * cosTheta), 0.f));
+    const SinCos sc = glibc_sincosf2(phi);
+    pdf = kInvTwoPi * rcp_cr(1.f - cosMax);
+    return world_at(cdir, mk(sinTheta * sc.c, sinTheta * sc.s, cosTheta));
+}
+
 enum : int {  // explicit-level steps between queries
     PS_ENTER,       // recursiveExplicit entry: Russian roulette (path.h:67-74)
     PS_IND_SAMPLE,  // indirect: sample the BSDF, trace (path.h:86-92)
@@ -194,6 +245,8 @@ enum : int {  // explicit-level steps between queries
     PS_RETURN,      // hand Lr to the caller level (path.h:106) or finish the sample
     PS_IMP_LEVEL,   // recursiveImplicit entry (path.h:36-44)
     PS_IMP_RETURN,  // Li * brdfCosTheta * (1.0 / pdf) up the implicit recursion
+    PS_DI_EMIT,     // direct integrator: next emitter / cosine sample
+    PS_DI_BSDF,     // direct integrator: next BSDF sample
     PS_WAIT,        // a query was issued
 };
 
@@ -318,6 +371,86 @@ __device__ void pt_advance(PtLane& L, int ps, f3 Lr, const PtParams& P, uint32_t
                 ps = PS_IMP_RETURN;
                 break;
             }
+            case PS_DI_EMIT: {  // renderArea / renderSolidAngle / renderCosineHemisphere / renderMIS
+                const int st = S.direct;
+                if (st == DI_BSDF) {
+                    ps = PS_DI_BSDF;
+                    break;
+                }
+                if (L.i >= S.emitter_samples) {
+                    if (st == DI_MIS) {
+                        if (S.emitter_samples != 0) L.eest = L.eest / static_cast<float>(S.emitter_samples);
+                        else L.eest = mk(0.f, 0.f, 0.f);
+                        L.i = 0;
+                        ps = PS_DI_BSDF;
+                        break;
+                    }
+                    pt_finish(L, P, L.ind / static_cast<float>(S.emitter_samples));  // Lr /= m_emitterSamples
+                    return;
+                }
+                L.i++;
+                if (st == DI_COSINE) {  // direct.h:214-229
+                    const f3 local = cosine_hemisphere(next2(L.rng));
+                    L.e_wil = local;
+                    L.ray = pt_ray(L.h.p, normalize(world_at(L.h.n, local)));
+                    L.q = PQ_DI_E;
+                    return;
+                }
+                float epdf;
+                const uint32_t n = static_cast<uint32_t>(sc.nemit);
+                uint32_t id = static_cast<uint32_t>(next1(L.rng) * static_cast<float>(n));  // selectEmitter
+                id = id < n - 1 ? id : n - 1;
+                epdf = 1.f / static_cast<float>(n);
+                const EmitterRecord& e = emitter_of(sc, static_cast<int>(id));
+                const f3 center = ld3(e.center);
+                const F2 u = next2(L.rng);
+                if (st == DI_AREA) {  // direct.h:160-190, sampleSphereByArea :94-107
+                    const f3 ne = uniform_sphere(u);
+                    const f3 pos = ne * e.radius + center;
+                    const f3 wiW = normalize(pos - L.h.p);
+                    const float pdf = 1.f / (((4 * kPi) * e.radius) * e.radius);
+                    const f3 dd = L.h.p - pos;
+                    const float d2 = dot(dd, dd);
+                    const float cosOut = dot(-wiW, ne);
+                    const f3 wil = local_at(L.h.n, wiW);
+                    if (cosOut <= 0.f || wil.z <= 0.f) break;
+                    L.e_id = static_cast<int>(id), L.e_pdf = epdf, L.e_apdf = pdf, L.e_wil = wil;
+                    L.e_cos = cosOut * rcp_cr(d2);  // areaToSolidAngle
+                    L.ray = Ray{L.h.p, wiW, kEpsilon, sqrt_cr(d2) - kEpsilon};
+                    L.q = PQ_DI_E;
+                    return;
+                }
+                float pdf;  // solid angle (direct.h:262-309) or MIS (:333-372)
+                const f3 wiW = sphere_solid_angle(u, L.h.p, center, e.radius, pdf);
+                const f3 wil = local_at(L.h.n, wiW);
+                if (wil.z <= 0.f) break;
+                L.e_id = static_cast<int>(id), L.e_pdf = epdf, L.e_apdf = pdf, L.e_wil = wil;
+                const f3 dc = center - L.h.p;
+                L.ray = Ray{L.h.p, wiW, kEpsilon, st == DI_SOLID_ANGLE ? sqrt_cr(dot(dc, dc)) + kEpsilon
+                                                                       : __builtin_inff()};
+                L.q = PQ_DI_E;
+                return;
+            }
+            case PS_DI_BSDF: {  // renderBSDF (direct.h:245-260) / renderMIS (:382-418)
+                if (L.i >= S.bsdf_samples) {
+                    if (S.direct == DI_BSDF) {
+                        pt_finish(L, P, L.ind / static_cast<float>(S.bsdf_samples));  // Lr /= m_bsdfSamples
+                        return;
+                    }
+                    if (S.bsdf_samples != 0) L.best = L.best / static_cast<float>(S.bsdf_samples);
+                    else L.best = mk(0.f, 0.f, 0.f);
+                    pt_finish(L, P, L.ind + (L.eest + L.best));  // Lr += emitterEstimator + bsdfEstimator
+                    return;
+                }
+                L.i++;
+                f3 wi;
+                float pdf;
+                L.b_f = bsdf_sample(bsdf_of(sc, L.h.mat), L.h.wo, next2(L.rng), wi, pdf);
+                L.b_pdf = pdf;
+                L.ray = pt_ray(L.h.p, world_at(L.h.n, wi));
+                L.q = PQ_DI_B;
+                return;
+            }
             default:
                 return;
         }
@@ -345,6 +478,11 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
             if (!is_zero(le)) return pt_finish(L, P, le);
             L.h = vis;
             L.depth = 0;
+            if (S.direct) {
+                L.i = 0;
+                L.ind = zero, L.eest = zero, L.best = zero;  // Lr, emitterEstimator, bsdfEstimator
+                return pt_advance(L, PS_DI_EMIT, zero, P, slot);
+            }
             return pt_advance(L, S.is_explicit ? PS_ENTER : PS_IMP_LEVEL, zero, P, slot);
         }
         case PQ_IND: {  // the do-while of path.h:82-95 and the recursion test of :98-108
@@ -421,6 +559,62 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
             const f3 Li = dot(vis.n, -L.wiw) > 0.f ? le : zero;
             return pt_advance(L, PS_IMP_RETURN, (Li * L.f) * rcp_cr(L.pdf), P, slot);
         }
+        case PQ_DI_E: {
+            const int st = S.direct;
+            const BsdfRecord& b = bsdf_of(sc, L.h.mat);
+            if (st == DI_COSINE) {  // direct.h:221-227
+                if (hit)
+                    L.ind = L.ind + (emission_of(sc, vis.mat) * bsdf_eval(b, L.e_wil, L.h.wo)) *
+                                        rcp_cr(cosine_hemisphere_pdf(L.e_wil));
+                return pt_advance(L, PS_DI_EMIT, zero, P, slot);
+            }
+            const EmitterRecord& e = emitter_of(sc, L.e_id);
+            if (st == DI_AREA) {  // direct.h:180-187: unoccluded up to the sampled point
+                if (!hit) {
+                    f3 c = ld3(e.radiance) * bsdf_eval(b, L.e_wil, L.h.wo);
+                    c = ((c * rcp_cr(L.e_apdf)) * rcp_cr(L.e_pdf)) * L.e_cos;
+                    L.ind = L.ind + c;
+                }
+                return pt_advance(L, PS_DI_EMIT, zero, P, slot);
+            }
+            // solid angle / MIS: the emitter's shape hit first, or nothing hit and the ray meets the sphere
+            const bool lit = hit ? vis.shape == e.shape : ray_sphere_hit(L.ray, ld3(e.center), e.radius);
+            if (lit) {
+                if (st == DI_SOLID_ANGLE) {  // direct.h:283-306
+                    const f3 c = (ld3(e.radiance) * bsdf_eval(b, L.e_wil, L.h.wo)) * rcp_cr(L.e_apdf);
+                    L.ind = L.ind + c * rcp_cr(L.e_pdf);
+                } else {  // direct.h:350-370
+                    const float bsdfPdf = bsdf_pdf(b, L.e_wil, L.h.wo);
+                    const float w = balance_heuristic(static_cast<float>(S.emitter_samples), L.e_apdf * L.e_pdf,
+                                                      static_cast<float>(S.bsdf_samples), bsdfPdf);
+                    const f3 c = ((ld3(e.radiance) * bsdf_eval(b, L.e_wil, L.h.wo)) * w) * rcp_cr(L.e_apdf);
+                    L.eest = L.eest + c * rcp_cr(L.e_pdf);
+                }
+            }
+            return pt_advance(L, PS_DI_EMIT, zero, P, slot);
+        }
+        case PQ_DI_B: {
+            if (hit) {
+                const f3 Le = emission_of(sc, vis.mat);
+                if (S.direct == DI_BSDF) {  // direct.h:253-256: Le * brdfCosTheta * (1.0 / pdf)
+                    L.ind = L.ind + (Le * L.b_f) * rcp_cr(L.b_pdf);
+                } else if (!is_zero(Le)) {  // direct.h:390-414
+                    const int eid = shape_emitter_of(sc, vis.shape);
+                    if (eid >= 0) {
+                        const EmitterRecord& e = emitter_of(sc, eid);
+                        const f3 dd = L.h.p - ld3(e.center);
+                        const float sin2 = e.radius * e.radius / dot(dd, dd);
+                        const float cosMax = sqrt_cr(glibc_fmaxf(0.f, 1.f - sin2));
+                        float esap = kInvTwoPi * rcp_cr(1.f - cosMax);
+                        esap = esap * (1.f / static_cast<float>(sc.nemit));
+                        const float w = balance_heuristic(static_cast<float>(S.bsdf_samples), L.b_pdf,
+                                                          static_cast<float>(S.emitter_samples), esap);
+                        L.best = L.best + ((Le * L.b_f) * w) * rcp_cr(L.b_pdf);
+                    }
+                }
+            }
+            return pt_advance(L, PS_DI_BSDF, zero, P, slot);
+        }
         default: return;
     }
 }
@@ -495,7 +689,7 @@ int pt_blocks_per_cu(size_t dyn_lds) {
     return n;
 }
 
-hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[7], float* fb,
+hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8], float* fb,
                      float4* levels, uint32_t* ring, uint2* gstack, uint32_t nslots, unsigned long long* work,
                      unsigned long long* counters, int grid, hipStream_t stream, void* dparams) {
     dev::PtParams host{};
@@ -508,6 +702,7 @@ hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int
     host.ps.emitter_samples = settings[4];
     host.ps.bsdf_samples = settings[5];
     host.ps.max_levels = settings[6];
+    host.ps.direct = settings[7];
     host.fb = fb, host.levels = levels, host.ring = ring, host.gstack = gstack, host.nslots = nslots;
     host.work = work, host.counters = counters;
     hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);

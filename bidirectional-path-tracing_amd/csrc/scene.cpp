@@ -674,6 +674,19 @@ bool build_device_layout(const HostScene& s, DeviceLayout& out, std::string& err
             out.emit_tri.push_back({q[3], q[4], q[5], q[6]});
             out.emit_tri.push_back({q[7], q[8], 0.f, 0.f});
         }
+        {  // shape center and "radius" (renderer.cpp:295-304, :349-353), float sums in corner order
+            float c[3] = {0.f, 0.f, 0.f}, maxx = -__builtin_inff();
+            for (int f = 0; f < r.nfaces; f++) {
+                const float* p = &s.pos[9 * static_cast<size_t>(s.shape_first[e.shape] + f)];
+                for (int k = 0; k < 3; k++) {
+                    for (int d = 0; d < 3; d++) c[d] = c[d] + p[3 * k + d];
+                    maxx = (maxx < p[3 * k]) ? p[3 * k] : maxx;  // std::max
+                }
+            }
+            const float n = static_cast<float>(3 * r.nfaces);
+            for (int d = 0; d < 3; d++) r.center[d] = c[d] / n;
+            r.radius = maxx - r.center[0];
+        }
         out.emit_cdf.insert(out.emit_cdf.end(), e.cdf.begin(), e.cdf.end());
         out.emitters.push_back(r);
     }

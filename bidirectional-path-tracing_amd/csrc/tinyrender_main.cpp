@@ -4,8 +4,9 @@
 // (main.cpp:146-152, "Render took: ... seconds.") -> Integrator::save, which
 // writes the EXR next to the TOML (integrator.cpp:26-30).
 //
-// Offline `type = "bdpt"` (the hot path) and `type = "path"` (the reference's
-// PathTracerIntegrator on the same substrate) are accepted; the other
+// Offline `type = "bdpt"` (the hot path), `type = "path"` and `type = "direct"`
+// (the reference's PathTracerIntegrator and DirectIntegrator on the same
+// substrate) are accepted; the other
 // integrators and the realtime render passes are rejected with an error.
 // Optional overrides (not in the reference): --width W --height H --spp N
 // --rr D --device K --out FILE.exr --seed S.
@@ -81,7 +82,8 @@ int main(int argc, char** argv) {
     }
     std::printf("%s\n", cfg.integrator);  // main.cpp:72
     const bool path = std::strcmp(cfg.integrator, "path") == 0;
-    if (!path && std::strcmp(cfg.integrator, "bdpt") != 0) {
+    const bool direct = std::strcmp(cfg.integrator, "direct") == 0;
+    if (!path && !direct && std::strcmp(cfg.integrator, "bdpt") != 0) {
         std::fprintf(stderr, "integrator type \"%s\" is not part of the MI355X BDPT path\n", cfg.integrator);
         return EXIT_FAILURE;
     }
@@ -113,6 +115,15 @@ int main(int argc, char** argv) {
         if (rr > 0) cfg.path.rr_depth = rr;
         p.rr_depth = 1;  // unused by the path tracer
         if (bdpt_render_path_host(ctx, &p, &cfg.path, rgb.data()) != BDPT_OK) return die("bdpt_render_path_host");
+    } else if (direct) {
+        p.rr_depth = 1;  // unused by the direct integrator
+        if (bdpt_render_direct_host(ctx, &p, &cfg.direct, rgb.data()) != BDPT_OK) {
+            if (cfg.direct.sampling_strategy == 0) {  // direct.h:460-461
+                std::printf("Error: wrong strategy\n");
+                return EXIT_FAILURE;
+            }
+            return die("bdpt_render_direct_host");
+        }
     } else if (bdpt_render_host(ctx, &p, rgb.data()) != BDPT_OK) {
         return die("bdpt_render_host");
     }

@@ -432,6 +432,8 @@ bool load_toml_config(const std::string& path, bdpt_config& cfg, std::string& er
     cfg.rr_prob = 0.f;
     cfg.spp = 1;
     cfg.path = bdpt_path_params{1, -1, 5, 0.95f, 1, 0};
+    cfg.direct = bdpt_direct_params{0, 1, 1};
+    copy_str(cfg.sampling_strategy, sizeof(cfg.sampling_strategy), "emitter");
     if (!cfg.realtime) {
         const std::string t = cfg.integrator;
         static const char* known[] = {"normal", "simple", "ao", "ro", "direct", "path", "bdpt"};
@@ -459,6 +461,18 @@ bool load_toml_config(const std::string& path, bdpt_config& cfg, std::string& er
             }
             cfg.path.rr_depth = cfg.rr_depth;
             cfg.path.rr_prob = cfg.rr_prob;
+        } else if (t == "direct") {  // main.cpp:88-92
+            if (!get_int(renderer, "emitterSamples", 1, cfg.direct.emitter_samples, err) ||
+                !get_int(renderer, "bsdfSamples", 1, cfg.direct.bsdf_samples, err))
+                return false;
+            if (cfg.direct.emitter_samples < 0 || cfg.direct.bsdf_samples < 0) {
+                err = "T cannot store negative value in get";
+                return false;
+            }
+            const Value* ss = find(renderer, "samplingStrategy");
+            copy_str(cfg.sampling_strategy, sizeof(cfg.sampling_strategy),
+                     (ss && ss->kind == Value::STRING) ? ss->s : "emitter");
+            cfg.direct.sampling_strategy = bdpt_direct_strategy(cfg.sampling_strategy);
         }
         if (!get_int(renderer, "spp", 1, cfg.spp, err)) return false;  // main.cpp:112
     }
@@ -466,6 +480,14 @@ bool load_toml_config(const std::string& path, bdpt_config& cfg, std::string& er
 }
 
 }  // namespace bdpt
+
+// DirectIntegrator::render's string dispatch (direct.h:450-461).
+extern "C" int32_t bdpt_direct_strategy(const char* name) {
+    static const char* names[] = {"area", "solidAngle", "cosineHemisphere", "bsdf", "mis"};
+    for (int32_t i = 0; name && i < 5; i++)
+        if (std::strcmp(name, names[i]) == 0) return i + 1;
+    return 0;
+}
 
 extern "C" int bdpt_config_load_toml(const char* toml_path, bdpt_config* out) {
     if (!toml_path || !out) return bdpt::set_error(BDPT_ERR_INVALID, "bdpt_config_load_toml: null argument");

@@ -24,6 +24,8 @@
  *   bdpt_render_path         PathTracerIntegrator::render     src/integrators/path.h:235-245 for every
  *                            (pixel, sample) of the offline loop (the reference's other offline
  *                            integrator, TOML type = "path"), on the same GPU substrate
+ *   bdpt_render_direct       DirectIntegrator::render         src/integrators/direct.h:449-462 (TOML
+ *                            type = "direct": area / solidAngle / cosineHemisphere / bsdf / mis)
  *
  * Conventions: plain C types only; status 0 = OK, < 0 = error (message from
  * bdpt_last_error(), thread-local). A context is bound to one HIP device and is
@@ -171,6 +173,30 @@ int bdpt_render_path(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_
 int bdpt_render_path_host(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_path_params* path,
                           float* fb_host);
 
+/* ---- the reference's direct-light integrator (src/integrators/direct.h) ---- */
+#define BDPT_DIRECT_AREA 1              /* samplingStrategy "area"             renderArea :143-195 */
+#define BDPT_DIRECT_SOLID_ANGLE 2       /* "solidAngle"                        renderSolidAngle :244-311 */
+#define BDPT_DIRECT_COSINE_HEMISPHERE 3 /* "cosineHemisphere"                  renderCosineHemisphere :198-233 */
+#define BDPT_DIRECT_BSDF 4              /* "bsdf"                              renderBSDF :235-264 */
+#define BDPT_DIRECT_MIS 5               /* "mis"                               renderMIS :313-447 */
+typedef struct {
+    int32_t sampling_strategy; /* BDPT_DIRECT_*; 0 = an unknown samplingStrategy string (rejected) */
+    int32_t emitter_samples;   /* [renderer] emitterSamples (default 1) */
+    int32_t bsdf_samples;      /* bsdfSamples (default 1) */
+} bdpt_direct_params;
+/* Renders every (pixel, sample) of the shard with DirectIntegrator::render and ADDS
+ * acc/spp per pixel to fb_device (conventions of bdpt_render_path). Emitters are the
+ * spheres the reference makes of them (center = the shape's vertex mean, radius =
+ * AABB max.x - center.x, renderer.cpp:295-304 / :349-358). An unknown strategy fails
+ * with BDPT_ERR_INVALID (the reference prints "Error: wrong strategy" and exits,
+ * direct.h:460-461). Asynchronous. */
+int bdpt_render_direct(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_direct_params* direct,
+                       float* fb_device, void* hip_stream);
+int bdpt_render_direct_host(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_direct_params* direct,
+                            float* fb_host);
+/* samplingStrategy string -> BDPT_DIRECT_* (0 when unknown). */
+int32_t bdpt_direct_strategy(const char* name);
+
 /* ---- scene configuration and image output (host only, no GPU needed) ---- */
 
 /* The settings loadTOML (src/main.cpp:22-116) reads from a scene .toml, with its
@@ -189,6 +215,8 @@ typedef struct {
     int32_t spp;             /* [renderer] spp (default 1) */
     bdpt_path_params path;   /* type = "path": isExplicit, maxDepth, rrDepth, rrProb, emitterSamples,
                                 bsdfSamples (main.cpp:96-101); defaults otherwise */
+    bdpt_direct_params direct;       /* type = "direct": emitterSamples, bsdfSamples (main.cpp:88-92) */
+    char sampling_strategy[32];      /* type = "direct": samplingStrategy as written (default "emitter") */
 } bdpt_config;
 
 /* loadTOML (main.cpp:22-116). BDPT_ERR_INVALID with the parse error otherwise. */

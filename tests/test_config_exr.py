@@ -74,6 +74,11 @@ def test_load_toml_matches_reference(path, expected):
                     got = {"isExplicit": int(sc.path.explicit), "maxDepth": sc.path.max_depth,
                            "emitterSamples": sc.path.emitter_samples, "bsdfSamples": sc.path.bsdf_samples}[k]
                     assert got == ref[k], k
+        if sc.integrator == "direct":  # main.cpp:88-92
+            d = sc.direct
+            assert (d.emitter_samples, d.bsdf_samples, d.sampling_strategy) == (
+                ref["emitterSamples"], ref["bsdfSamples"], ref["samplingStrategy"])
+            assert d.c().sampling_strategy == bdpt_amd.DIRECT_STRATEGIES.get(ref["samplingStrategy"], 0)
         assert c.spp == ref["spp"]
         if "rrDepth" in ref:
             assert c.rr_depth == ref["rrDepth"]
