@@ -290,8 +290,12 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
         c->sc.lds_emit_off = up4(nb);
         c->sc.lds_shape_off = up4(c->sc.lds_emit_off + static_cast<uint32_t>(L.emitters.size() * sizeof(EmitterRecord) / 4));
         c->sc.lds_words = up4(c->sc.lds_shape_off + static_cast<uint32_t>(L.shape_emitter.size()));
+        if (c->sc.lds_words * 4u > 24u * 1024u) {  // many shapes: their emitter map stays in HBM
+            c->sc.lds_words = c->sc.lds_shape_off;
+            c->sc.lds_shape_off = dev::kNoLds;
+        }
         if (c->sc.lds_words * 4u > 24u * 1024u)
-            return fail(BDPT_ERR_UNSUPPORTED, "BSDF / emitter / shape tables exceed the 24 KiB LDS budget");
+            return fail(BDPT_ERR_UNSUPPORTED, "BSDF / emitter tables exceed the 24 KiB LDS budget");
         // Emitter faces + CDFs join the LDS tables when that costs no resident block.
         c->sc.lds_etri_off = c->sc.lds_ecdf_off = dev::kNoLds;
         c->sc.n_etri = static_cast<int32_t>(L.emit_tri.size() / 5);

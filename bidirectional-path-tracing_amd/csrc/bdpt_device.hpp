@@ -63,7 +63,7 @@ constexpr uint32_t kNoLds = 0xffffffffu;
 // map — live in the kernels' dynamic LDS: the divergent shading code reads
 // them with ds_read instead of chains of dependent global loads. Layout (words):
 // [0, emit_off) BsdfRecord[nbsdf], [emit_off, shape_off) EmitterRecord[nemit],
-// [shape_off, ...) int32 shape_emitter[nshapes]; anything a kernel keeps in
+// [shape_off, ...) int32 shape_emitter[nshapes] (unless kNoLds); anything a kernel keeps in
 // dynamic LDS besides goes at lds_words.
 extern __shared__ uint32_t g_scene_lds[];
 __device__ __forceinline__ const BsdfRecord& bsdf_of(const DevScene&, int m) {
@@ -72,7 +72,10 @@ __device__ __forceinline__ const BsdfRecord& bsdf_of(const DevScene&, int m) {
 __device__ __forceinline__ const EmitterRecord& emitter_of(const DevScene& sc, int i) {
     return reinterpret_cast<const EmitterRecord*>(g_scene_lds + sc.lds_emit_off)[i];
 }
+// The shape -> emitter map stays in global memory when a scene has too many
+// shapes for the LDS budget (lds_shape_off == kNoLds; read on emitter hits only).
 __device__ __forceinline__ int shape_emitter_of(const DevScene& sc, int shape) {
+    if (sc.lds_shape_off == kNoLds) return *(const __attribute__((address_space(1))) int32_t*)(sc.shape_emitter + shape);
     return static_cast<int>(g_scene_lds[sc.lds_shape_off + shape]);
 }
 // Cooperative copy by the whole block, then a barrier.
@@ -84,8 +87,9 @@ __device__ __forceinline__ void scene_tables_to_lds(const DevScene& sc) {
     const uint32_t* m = reinterpret_cast<const uint32_t*>(sc.shape_emitter);
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) g_scene_lds[i] = b[i];
     for (uint32_t i = threadIdx.x; i < ne; i += blockDim.x) g_scene_lds[sc.lds_emit_off + i] = e[i];
-    for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(sc.nshapes); i += blockDim.x)
-        g_scene_lds[sc.lds_shape_off + i] = m[i];
+    if (sc.lds_shape_off != kNoLds)
+        for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(sc.nshapes); i += blockDim.x)
+            g_scene_lds[sc.lds_shape_off + i] = m[i];
     if (sc.lds_etri_off != kNoLds) {
         const uint32_t* t = reinterpret_cast<const uint32_t*>(sc.emit_tri);
         const uint32_t* c = reinterpret_cast<const uint32_t*>(sc.emit_cdf);
