@@ -38,6 +38,11 @@ hipError_t wf_launch_pass(const void* dparams, uint32_t flags, uint32_t nslots, 
                           uint32_t p_lds_words, int64_t pass, hipStream_t stream);
 int wf_parts();
 int frame_kernel_blocks_per_cu(size_t dyn_lds);
+// bdpt_kernels_deep.hip: the same megakernel for rrDepth > 28
+hipError_t launch_frame_deep(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf,
+                             uint2* gstack, uint32_t nslots, unsigned long long* work, unsigned long long* counters,
+                             int grid, hipStream_t stream, void* dparams);
+int frame_kernel_blocks_per_cu_deep(size_t dyn_lds);
 size_t pt_params_bytes();
 int pt_blocks_per_cu(size_t dyn_lds);
 hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8], float* fb,
@@ -63,7 +68,8 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess) return fail(BDPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int kMaxRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
+constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
+constexpr int kMaxRrDepth = 1024;  // beyond 28 the megakernel continues MT19937 from an HBM ring
 }  // namespace
 
 // Error reporting shared with the other C-ABI translation units (exr_io.cpp, toml_config.cpp).
@@ -118,6 +124,7 @@ struct bdpt_ctx {
     float4* pt_levels = nullptr;
     size_t pt_levels_f4 = 0;
     uint32_t* pt_ring = nullptr;
+    uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28)
     void* pt_dparams = nullptr;
     // stats of the last render
     bool pending_timing = false;
@@ -232,7 +239,8 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
                     static_cast<void*>(c->wf_res), static_cast<void*>(c->wf_wctr), static_cast<void*>(c->wf_tctr),
                     static_cast<void*>(c->sstack), c->wf_dparams,
                     static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams,
-                    static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams})
+                    static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
+                    static_cast<void*>(c->mt_ring)})
         if (p) (void)hipFree(p);
     if (c->host_ctr) (void)hipHostFree(c->host_ctr);
     for (hipEvent_t e : c->chunk_ev)
@@ -281,13 +289,15 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     if ((rc = upload(c.get(), L.shape_emitter.data(), L.shape_emitter.size() * 4, &p))) return rc;
     c->sc.shape_emitter = static_cast<const int32_t*>(p);
     c->sc.root_link = L.root_link;
+    c->sc.mt_ring = nullptr;
+    c->sc.mt_ring_stride = 0;
     c->sc.nemit = static_cast<int32_t>(L.emitters.size());
     c->sc.nbsdf = static_cast<int32_t>(L.bsdfs.size());
     c->sc.nshapes = static_cast<int32_t>(L.shape_emitter.size());
     {  // LDS table layout (bdpt_device.hpp scene_tables_to_lds), 16-byte aligned parts
         auto up4 = [](uint32_t w) { return (w + 3u) & ~3u; };
         const uint32_t nb = static_cast<uint32_t>(L.bsdfs.size() * sizeof(BsdfRecord) / 4);
-        c->sc.lds_emit_off = up4(nb);
+        c->sc.lds_emit_off = up4(dev::kLdsHdr + nb);
         c->sc.lds_shape_off = up4(c->sc.lds_emit_off + static_cast<uint32_t>(L.emitters.size() * sizeof(EmitterRecord) / 4));
         c->sc.lds_words = up4(c->sc.lds_shape_off + static_cast<uint32_t>(L.shape_emitter.size()));
         if (c->sc.lds_words * 4u > 24u * 1024u) {  // many shapes: their emitter map stays in HBM
@@ -346,7 +356,10 @@ static int check_params(const bdpt_frame_params* p) {
     if (static_cast<int64_t>(p->width) * p->height >= (1ll << 31))
         return fail(BDPT_ERR_INVALID, "image too large (W*H must fit int32, as in the reference)");
     if (p->rr_depth < 1 || p->rr_depth > kMaxRrDepth)
-        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth must be in [1, 28] (lazy MT19937 window)");
+        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth must be in [1, 1024]");
+    if (p->rr_depth > kLazyRrDepth && (p->flags & BDPT_FLAG_WAVEFRONT))
+        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 needs the megakernel schedule (the wavefront schedule "
+                                          "keeps the lazy MT19937 window only)");
     if (p->strategy < 0 || p->strategy > 2) return fail(BDPT_ERR_INVALID, "unknown strategy");
     if (p->row_stride < 1 || p->row_offset < 0) return fail(BDPT_ERR_INVALID, "bad row shard");
     return BDPT_OK;
@@ -455,14 +468,27 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     const dev::DevFrame fr = make_frame(p);
     const bool mega = (p->flags & BDPT_FLAG_WAVEFRONT) == 0;
     if (mega && (rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
+    dev::DevScene sc = c->sc;
+    if (mega && p->rr_depth > kLazyRrDepth) {  // draws past 226: the lanes' MT19937 rings
+        if (!c->mt_ring) HIP_TRY(hipMalloc(&c->mt_ring, sizeof(uint32_t) * 624 * static_cast<size_t>(c->nslots)));
+        sc.mt_ring = c->mt_ring;
+        sc.mt_ring_stride = c->nslots;
+    }
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
     int64_t launches = 0;
     if (fr.total_samples > 0) {
         if (mega) {
-            HIP_TRY(launch_frame(c->sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
-                                 c->dparams));
+            if (p->rr_depth > kLazyRrDepth) {  // never more resident blocks than the slots allocated
+                const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_deep(
+                                                               4 * static_cast<size_t>(c->sc.lds_words)));
+                HIP_TRY(launch_frame_deep(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
+                                          c->dparams));
+            } else {
+                HIP_TRY(launch_frame(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
+                                     c->dparams));
+            }
             launches = 1;
         } else {
             int64_t passes = 0;

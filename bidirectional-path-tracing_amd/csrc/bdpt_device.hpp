@@ -56,18 +56,23 @@ struct DevScene {
     // costing a resident block (host decision); kNoLds otherwise
     uint32_t lds_etri_off, lds_ecdf_off;
     int32_t n_etri, n_ecdf;
+    // MT19937 continuation ring of the megakernel's lanes (rrDepth > 28): word k
+    // of lane slot s at mt_ring[k * mt_ring_stride + s]; null otherwise
+    uint32_t* mt_ring;
+    uint32_t mt_ring_stride;
 };
 constexpr uint32_t kNoLds = 0xffffffffu;
+constexpr uint32_t kLdsHdr = 4;  // LDS header words: mt_ring (2 words), mt_ring_stride, unused
 
 // Small per-scene tables — BSDF records, emitter records, shape -> emitter
 // map — live in the kernels' dynamic LDS: the divergent shading code reads
 // them with ds_read instead of chains of dependent global loads. Layout (words):
-// [0, emit_off) BsdfRecord[nbsdf], [emit_off, shape_off) EmitterRecord[nemit],
+// [0, kLdsHdr) header, [kLdsHdr, emit_off) BsdfRecord[nbsdf], [emit_off, shape_off) EmitterRecord[nemit],
 // [shape_off, ...) int32 shape_emitter[nshapes] (unless kNoLds); anything a kernel keeps in
 // dynamic LDS besides goes at lds_words.
 extern __shared__ uint32_t g_scene_lds[];
 __device__ __forceinline__ const BsdfRecord& bsdf_of(const DevScene&, int m) {
-    return reinterpret_cast<const BsdfRecord*>(g_scene_lds)[m];
+    return reinterpret_cast<const BsdfRecord*>(g_scene_lds + kLdsHdr)[m];
 }
 __device__ __forceinline__ const EmitterRecord& emitter_of(const DevScene& sc, int i) {
     return reinterpret_cast<const EmitterRecord*>(g_scene_lds + sc.lds_emit_off)[i];
@@ -85,7 +90,14 @@ __device__ __forceinline__ void scene_tables_to_lds(const DevScene& sc) {
     const uint32_t* b = reinterpret_cast<const uint32_t*>(sc.bsdf);
     const uint32_t* e = reinterpret_cast<const uint32_t*>(sc.emit);
     const uint32_t* m = reinterpret_cast<const uint32_t*>(sc.shape_emitter);
-    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) g_scene_lds[i] = b[i];
+    if (threadIdx.x == 0) {
+        const uint64_t ring = reinterpret_cast<uint64_t>(sc.mt_ring);
+        g_scene_lds[0] = static_cast<uint32_t>(ring);
+        g_scene_lds[1] = static_cast<uint32_t>(ring >> 32);
+        g_scene_lds[2] = sc.mt_ring_stride;
+        g_scene_lds[3] = 0u;
+    }
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) g_scene_lds[kLdsHdr + i] = b[i];
     for (uint32_t i = threadIdx.x; i < ne; i += blockDim.x) g_scene_lds[sc.lds_emit_off + i] = e[i];
     if (sc.lds_shape_off != kNoLds)
         for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(sc.nshapes); i += blockDim.x)
@@ -129,7 +141,8 @@ struct Hit {
 // sample draws at most 10 + 8 (rrDepth - 1) numbers (< 227 for rrDepth <= 28),
 // all from the first twist, so output n is computed lazily from the seeding
 // recurrence: out_n = temper(x[n+397] ^ twist(x[n], x[n+1])). State: x[n],
-// x[n+1], x[n+397] and n.
+// x[n+1], x[n+397] and n. Draws past 226 continue from a per-lane ring of 624
+// untempered outputs in HBM (mt_ring_step), which only deeper rrDepth needs.
 struct LazyMT {
     uint32_t a0, a1, b, n;
 };
@@ -180,9 +193,91 @@ __device__ __forceinline__ uint32_t mt_next_u32(LazyMT& r) {
     return v;
 }
 
+__device__ __forceinline__ uint32_t mt_temper(uint32_t v) {
+    v ^= (v >> 11);
+    v ^= (v << 7) & 0x9d2c5680u;
+    v ^= (v << 15) & 0xefc60000u;
+    v ^= (v >> 18);
+    return v;
+}
+__device__ __forceinline__ uint32_t mt_twist(uint32_t a, uint32_t b, uint32_t c) {  // c ^ twist(a, b)
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// Output n >= 227 of std::mt19937(seed): u[n] = u[n-227] ^ twist(u[n-624],
+// u[n-623]) (with the seeding values x[n], x[n+1] while n + 1 < 624), kept in a
+// 624-word ring (word k at ring[k * st]). The first call materialises outputs
+// 0..226 (the seed is needed then only).
+__device__ __forceinline__ uint32_t mt_ring_step(LazyMT& m, uint32_t seed, uint32_t* ring, uint32_t st) {
+    const uint32_t n = m.n;
+    if (n == 227) {
+        LazyMT t;
+        t.a0 = seed;
+        t.a1 = mt_init_step(seed, 1);
+        t.b = seed;
+        for (uint32_t i = 1; i <= 397; i++) t.b = mt_init_step(t.b, i);
+        for (uint32_t k = 0; k < 227; k++) {
+            ring[k * st] = mt_twist(t.a0, t.a1, t.b);
+            t.a0 = t.a1;
+            t.a1 = mt_init_step(t.a1, k + 2);
+            t.b = mt_init_step(t.b, k + 398);
+        }
+    }
+    uint32_t un, un1;
+    if (n < 623) un = m.a0, un1 = m.a1;
+    else if (n == 623) un = m.a0, un1 = ring[0];
+    else un = ring[((n - 624) % 624) * st], un1 = ring[((n - 623) % 624) * st];
+    const uint32_t v = mt_twist(un, un1, ring[((n - 227) % 624) * st]);
+    ring[(n % 624) * st] = v;
+    if (n + 2 <= 623) {
+        m.a0 = m.a1;
+        m.a1 = mt_init_step(m.a1, n + 2);
+    } else if (n + 1 <= 623) {
+        m.a0 = m.a1;
+    }
+    m.n = n + 1;
+    return mt_temper(v);
+}
+
+// x[0] (the seed) from x[i]: the seeding step x -> 1812433253 (x ^ x >> 30) + i
+// is a bijection (odd multiplier; a 30-bit xorshift undoes itself).
+__device__ __forceinline__ uint32_t mt_seed_from(uint32_t x, uint32_t i) {
+    constexpr uint32_t kInv = 0x9638806du;  // 1812433253^-1 mod 2^32
+    for (; i >= 1; i--) {
+        x = (x - i) * kInv;
+        x ^= x >> 30;
+    }
+    return x;
+}
+
+#ifndef BDPT_DEEP_RNG
+#define BDPT_DEEP_RNG 0  // 1: the deep-path build of the megakernel (bdpt_kernels_deep.hip)
+#endif
+#if BDPT_DEEP_RNG
+// BDPT draw n >= 227 (rrDepth > 28: the deep build of the megakernel; the
+// host refuses such depths elsewhere). The ring of this lane slot is found
+// through the LDS header. Only this build carries the branch and the call at
+// every draw site: in the default build they cost ~30 % of the throughput.
+__device__ BDPT_NOINLINE uint32_t mt_u32_long(LazyMT& r) {
+    const uint64_t base = (static_cast<uint64_t>(g_scene_lds[1]) << 32) | g_scene_lds[0];
+    uint32_t* const ring = reinterpret_cast<uint32_t*>(base);
+    if (!ring) return mt_next_u32(r);  // unreachable (host check)
+    const uint32_t st = g_scene_lds[2];
+    const uint32_t seed = r.n == 227 ? mt_seed_from(r.a0, 227) : 0u;
+    return mt_ring_step(r, seed, ring + (blockIdx.x * blockDim.x + threadIdx.x), st);
+}
+
+#endif
+
 // generate_canonical<float, 24> (libstdc++ 11 random.tcc:3348-3380).
 __device__ __forceinline__ float next1(LazyMT& r) {
-    float f = static_cast<float>(mt_next_u32(r)) / 4294967296.0f;
+#if BDPT_DEEP_RNG
+    const uint32_t u = r.n < 227 ? mt_next_u32(r) : mt_u32_long(r);
+#else
+    const uint32_t u = mt_next_u32(r);
+#endif
+    float f = static_cast<float>(u) / 4294967296.0f;
     return f >= 1.0f ? 0x1.fffffep-1f : f;
 }
 struct F2 {

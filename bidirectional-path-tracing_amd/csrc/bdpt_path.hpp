@@ -17,7 +17,10 @@ namespace dev {
 
 constexpr int kLvFields = 16;    // p vcm n vc wo rr tp mat
 constexpr uint32_t kFlagNoEyeAccum = 0x100u;  // single-sample API: Li is returned, not added
-constexpr int kMaxStepsPerSample = 4096;      // safety bound (a legal sample needs < 900 at rrDepth 28)
+// Safety bound on the queries of one sample: a legal sample issues at most D
+// light-walk rays, D camera splats, D eye-walk rays and, per eye vertex, one
+// light sample plus D - 1 connections: < (D + 3)(D + 1) for rrDepth D.
+__device__ __forceinline__ int max_steps_per_sample(int rr_depth) { return (rr_depth + 3) * (rr_depth + 1) + 64; }
 
 // Light-vertex scratch, one contiguous record per lane: vertex v of slot s is
 // the four float4 at lv[(s * maxv + v) * 4 + q] — (p, vcm) (n, vc) (wo, rr)
@@ -589,7 +592,7 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
         default: act = A_DONE;
     }
     // A state-machine bug must not hang the GPU: bound the queries per sample.
-    if (++L.c.steps > kMaxStepsPerSample && act != A_FINISH) act = A_FINISH;
+    if (++L.c.steps > max_steps_per_sample(fr.rr_depth) && act != A_FINISH) act = A_FINISH;
     return act;
 }
 

@@ -32,49 +32,8 @@ struct PtRng {
     uint32_t stride;
 };
 
-__device__ __forceinline__ uint32_t mt_temper(uint32_t v) {
-    v ^= (v >> 11);
-    v ^= (v << 7) & 0x9d2c5680u;
-    v ^= (v << 15) & 0xefc60000u;
-    v ^= (v >> 18);
-    return v;
-}
-__device__ __forceinline__ uint32_t mt_twist(uint32_t a, uint32_t b, uint32_t c) {  // c ^ twist(a, b)
-    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-}
-
-// Output n >= 227 of std::mt19937(seed): from the ring (and the seeding
-// iterators while n + 1 < 624). The first call materialises outputs 0..226.
-__device__ BDPT_NOINLINE uint32_t pt_u32_slow(PtRng& r) {
-    const uint32_t n = r.m.n;
-    uint32_t* ring = r.ring;
-    const uint32_t st = r.stride;
-    if (n == 227) {
-        LazyMT t;
-        mt_seed(t, r.seed);
-        for (uint32_t k = 0; k < 227; k++) {
-            ring[k * st] = mt_twist(t.a0, t.a1, t.b);
-            t.a0 = t.a1;
-            t.a1 = mt_init_step(t.a1, k + 2);
-            t.b = mt_init_step(t.b, k + 398);
-        }
-    }
-    uint32_t un, un1;
-    if (n < 623) un = r.m.a0, un1 = r.m.a1;
-    else if (n == 623) un = r.m.a0, un1 = ring[0];
-    else un = ring[((n - 624) % 624) * st], un1 = ring[((n - 623) % 624) * st];
-    const uint32_t v = mt_twist(un, un1, ring[((n - 227) % 624) * st]);
-    ring[(n % 624) * st] = v;
-    if (n + 2 <= 623) {
-        r.m.a0 = r.m.a1;
-        r.m.a1 = mt_init_step(r.m.a1, n + 2);
-    } else if (n + 1 <= 623) {
-        r.m.a0 = r.m.a1;
-    }
-    r.m.n = n + 1;
-    return mt_temper(v);
-}
+// Output n >= 227 of std::mt19937(seed) from the lane's ring (mt_ring_step).
+__device__ BDPT_NOINLINE uint32_t pt_u32_slow(PtRng& r) { return mt_ring_step(r.m, r.seed, r.ring, r.stride); }
 __device__ __forceinline__ float next1(PtRng& r) {
     const uint32_t u = r.m.n < 227 ? mt_next_u32(r.m) : pt_u32_slow(r);
     const float f = static_cast<float>(u) / 4294967296.0f;  // generate_canonical (random.tcc:3348-3380)

@@ -84,7 +84,8 @@ typedef struct {
     bdpt_camera camera;
     int32_t width, height; /* [film] (the global image; shards still splat into it) */
     int32_t spp;           /* [renderer] spp */
-    int32_t rr_depth;      /* [renderer] rrDepth: hard path-depth cap (NO_RR=1, bdpt.h:18) */
+    int32_t rr_depth;      /* [renderer] rrDepth: hard path-depth cap (NO_RR=1, bdpt.h:18); 1..1024
+                              (1..28 with BDPT_FLAG_WAVEFRONT and bdpt_render_sample) */
     int32_t strategy;      /* BDPT_STRATEGY_* (reference default: BDPT) */
     uint32_t seed_base;    /* 260450963 = the reference's Sampler seed (renderer.cpp:155) */
     int32_t row_offset;    /* shard: render rows row_offset, row_offset+row_stride, ... */

@@ -102,9 +102,30 @@ def test_gpu_matches_oracle_other_configs(name, W, H, spp, rr):
     assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
 
 
-def test_gpu_rr_depth_beyond_lazy_window_is_refused():
-    """rrDepth 29 can need 234 draws > 227: an error, never a wrong image."""
+@pytest.mark.parametrize("rr,W,H,spp", [(29, 16, 12, 2), (40, 16, 12, 2), (150, 12, 8, 2), (300, 8, 6, 2)])
+def test_gpu_deep_rr_depth_continues_mt19937_from_ring(rr, W, H, spp, tmp_path):
+    """rrDepth > 28 in a closed box (every path runs to rrDepth): samples draw
+    past the lazy window (227) and, from rrDepth ~80, past a full MT19937 state
+    (624): the megakernel continues from the lanes' HBM rings, same image as
+    the oracle's real std::mt19937 restatement."""
+    obj = variants.closed_box_obj(str(tmp_path))
+    cam = variants.CLOSED_CAMERA
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**cam), width=W, height=H, spp=spp, rr_depth=rr)
+    fb = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(obj), cfg).render_frame().reshape(-1)
+    O.counters(True)
+    ref, n = O.Scene(obj).render(O.make_params(cam, W, H, spp, rr))
+    draws = O.counters(True)["rng_draws"] / n
+    assert draws > {29: 150, 40: 200, 150: 550, 300: 900}[rr]  # mean draws per sample: many past 227 / 624
+    worst, exact, _ = report(fb, ref.reshape(-1))
+    assert worst <= TOL, f"rr={rr}: max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
+
+
+def test_gpu_rr_depth_limits():
+    """The wavefront schedule keeps the lazy window (rrDepth <= 28); past 1024 is refused."""
     it = integrator("cbox_low", 8, 8, 1, 29)
+    with pytest.raises(bdpt_amd.BdptError, match="rr_depth"):
+        it.render_frame(flags=bdpt_amd.FLAG_WAVEFRONT)
+    it = integrator("cbox_low", 8, 8, 1, 1025)
     with pytest.raises(bdpt_amd.BdptError, match="rr_depth"):
         it.render_frame()
 

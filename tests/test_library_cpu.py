@@ -19,7 +19,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_symbols():
     with open(os.path.join(REPO, "include", "bdpt_amd.h")) as f:
         text = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(bdpt_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|const char\*)\s+(bdpt_\w+)\s*\(", text, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
