@@ -512,9 +512,14 @@ constexpr int kPtMaxLevels = 512;  // recursion levels per lane under Russian ro
 static int ensure_pt(bdpt_ctx* c, int levels) {
     if (!c->pt_dparams) {
         HIP_TRY(hipMalloc(&c->pt_dparams, pt_params_bytes()));
-        // At most 2 resident 256-lane blocks per CU, within the BDPT grid (the
+        // Up to 4 resident 256-lane blocks per CU (4 waves/SIMD at 128 VGPRs;
+        // measured 70 -> 119 Msamples/s from 2), within the BDPT grid (the
         // traversal-stack overflow buffer is sized for that many slots).
-        c->pt_grid = std::min(c->grid, c->cus * std::min(2, pt_blocks_per_cu(4 * static_cast<size_t>(c->sc.lds_words))));
+        // BDPT_PT_BLOCKS overrides the cap (experiments). Level stacks: 512 x 80 B
+        // per slot, ~10.7 GB at 256 CUs x 1024 slots under Russian roulette.
+        const char* cap_env = std::getenv("BDPT_PT_BLOCKS");
+        const int cap = cap_env ? std::max(1, std::atoi(cap_env)) : 4;
+        c->pt_grid = std::min(c->grid, c->cus * std::min(cap, pt_blocks_per_cu(4 * static_cast<size_t>(c->sc.lds_words))));
         c->pt_nslots = static_cast<uint32_t>(c->pt_grid) * 256u;
         HIP_TRY(hipMalloc(&c->pt_ring, sizeof(uint32_t) * 624 * static_cast<size_t>(c->pt_nslots)));
     }

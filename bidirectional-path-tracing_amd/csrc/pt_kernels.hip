@@ -210,7 +210,18 @@ enum : int {  // explicit-level steps between queries
 };
 
 // Runs the lane from step `ps` until it issues a query or finishes its sample.
-__device__ void pt_advance(PtLane& L, int ps, f3 Lr, const PtParams& P, uint32_t slot) {
+#ifndef PT_INLINE_ADVANCE
+#define PT_INLINE_ADVANCE 1  // pt_advance inlined: the lane state stays in registers (not scratch)
+#endif
+#ifndef PT_WAVES_PER_EU
+#define PT_WAVES_PER_EU 4  // 128 VGPRs, 4 blocks of 256 lanes per CU
+#endif
+#if PT_INLINE_ADVANCE
+__device__ __forceinline__
+#else
+__device__
+#endif
+void pt_advance(PtLane& L, int ps, f3 Lr, const PtParams& P, uint32_t slot) {
     const DevScene& sc = P.sc;
     const PtSettings& S = P.ps;
     for (int guard = 0; guard < 1 << 20; guard++) {
@@ -579,7 +590,7 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
 }
 
 template <bool COUNT>
-__global__ __launch_bounds__(256) void pt_frame_kernel(const PtParams* __restrict__ pp) {
+__global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const PtParams* __restrict__ pp) {
     const PtParams& P = *pp;
     __shared__ uint2 stack_mem[kLdsStack * 256];
     scene_tables_to_lds(P.sc);
