@@ -128,6 +128,7 @@ def lib():
         L.bdpt_render_direct_host.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_DirectParams), vp]
         L.bdpt_direct_strategy.restype = i32
         L.bdpt_direct_strategy.argtypes = [ctypes.c_char_p]
+        L.bdpt_debug_math.argtypes = [i32, i32, vp, vp, vp, ctypes.c_int64]
         L.bdpt_encode_exr.argtypes = [vp, i32, i32, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         L.bdpt_save_exr.argtypes = [vp, i32, i32, ctypes.c_char_p]
         _lib = L
@@ -437,3 +438,15 @@ class DirectIntegrator(BDPTIntegrator):
         p, d = self.params(row_offset, row_stride, flags), self.direct.c()
         _check(lib().bdpt_render_direct(self._h, ctypes.byref(p), ctypes.byref(d), ctypes.c_void_p(fb_ptr),
                                         ctypes.c_void_p(stream_ptr)))
+
+
+def debug_math(fn: str, x: np.ndarray, y: np.ndarray | None = None, device: int = 0) -> np.ndarray:
+    """The device sinf / cosf / powf (glibc restatements) on float32 inputs:
+    fn in {"sinf", "cosf", "powf", "sincos_s", "sincos_c"}."""
+    code = {"sinf": 0, "cosf": 1, "powf": 2, "sincos_s": 3, "sincos_c": 4}[fn]
+    x = np.ascontiguousarray(x, np.float32)
+    yy = None if y is None else np.ascontiguousarray(y, np.float32)
+    out = np.empty_like(x)
+    _check(lib().bdpt_debug_math(device, code, x.ctypes.data, None if yy is None else yy.ctypes.data,
+                                 out.ctypes.data, x.size))
+    return out

@@ -50,6 +50,7 @@ hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int
                      unsigned long long* counters, int grid, hipStream_t stream, void* dparams);
 int frame_kernel_block();
 int light_vertex_fields();
+hipError_t launch_math_check(int32_t fn, const float* x, const float* y, float* out, int64_t n, hipStream_t st);
 }  // namespace bdpt
 
 using namespace bdpt;
@@ -629,6 +630,28 @@ int bdpt_render_direct_host(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_
     if ((rc = bdpt_render_direct(c, p, d, c->tmp_fb, c->stream))) return rc;
     HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_debug_math(int32_t device, int32_t fn, const float* x, const float* y, float* out, int64_t n) {
+    if (!x || !out || n < 0 || (fn == 2 && !y) || fn < 0 || fn > 4) return fail(BDPT_ERR_INVALID, "bad argument");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(BDPT_ERR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= count) return fail(BDPT_ERR_INVALID, "bad device");
+    HIP_TRY(hipSetDevice(device));
+    if (n == 0) return BDPT_OK;
+    float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    const size_t bytes = sizeof(float) * static_cast<size_t>(n);
+    hipError_t e = hipMalloc(&dx, bytes);
+    if (e == hipSuccess) e = hipMalloc(&dy, bytes);
+    if (e == hipSuccess) e = hipMalloc(&dout, bytes);
+    if (e == hipSuccess) e = hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dy, y ? y : x, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_math_check(fn, dx, dy, dout, n, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+    for (float* p : {dx, dy, dout})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(BDPT_ERR_HIP, std::string("bdpt_debug_math: ") + hipGetErrorString(e));
     return BDPT_OK;
 }
 

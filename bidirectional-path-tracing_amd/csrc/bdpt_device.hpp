@@ -939,7 +939,14 @@ __device__ __forceinline__ float fresnel_dielectric(float eta_i, float eta_t, fl
 }
 
 // BSDF::sample: sets wi, returns f*cos, writes the solid-angle pdf.
+#ifndef BDPT_SAMPLE_STRUCT
+#define BDPT_SAMPLE_STRUCT 1
+#endif
+#if BDPT_SAMPLE_STRUCT
+__device__ __forceinline__ f3 bsdf_sample_body(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
+#else
 __device__ BDPT_NOINLINE f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
+#endif
     switch (b.kind) {
         case BSDF_MIRROR:  // perfectmirror.h:49-59
             pdf = 1.f;
@@ -995,6 +1002,25 @@ __device__ BDPT_NOINLINE f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f
             return mk(0.f, 0.f, 0.f);
     }
 }
+#if BDPT_SAMPLE_STRUCT
+// The call returns everything by value (in VGPRs): with reference outputs the
+// caller's wi / pdf went through scratch around every call.
+struct BsdfSample {
+    f3 f, wi;
+    float pdf;
+};
+__device__ BDPT_NOINLINE BsdfSample bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u) {
+    BsdfSample s;
+    s.f = bsdf_sample_body(b, wo, u, s.wi, s.pdf);
+    return s;
+}
+__device__ __forceinline__ f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
+    const BsdfSample s = bsdf_sample_call(b, wo, u);
+    wi = s.wi;
+    pdf = s.pdf;
+    return s.f;
+}
+#endif
 __device__ __forceinline__ f3 bsdf_sample(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
     if (b.kind == BSDF_DIFFUSE) {  // diffuse.h:52-61
         wi = cosine_hemisphere(u);

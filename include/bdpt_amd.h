@@ -198,6 +198,13 @@ int bdpt_render_direct_host(bdpt_ctx* ctx, const bdpt_frame_params* params, cons
 /* samplingStrategy string -> BDPT_DIRECT_* (0 when unknown). */
 int32_t bdpt_direct_strategy(const char* name);
 
+/* ---- diagnostics ---- */
+/* The device restatements of glibc's transcendental functions the path uses
+ * (std::sinf / cosf / powf in src/core/math.h:125-242, mixture.h:70), element-wise
+ * on device `device`: fn 0 sinf(x), 1 cosf(x), 2 powf(x, y), 3 / 4 the sin / cos
+ * of the fused sincos the warps call. Host arrays of n floats; synchronous. */
+int bdpt_debug_math(int32_t device, int32_t fn, const float* x, const float* y, float* out, int64_t n);
+
 /* ---- scene configuration and image output (host only, no GPU needed) ---- */
 
 /* The settings loadTOML (src/main.cpp:22-116) reads from a scene .toml, with its

@@ -10,5 +10,5 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -
 /opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/bdpt_kernels.hip -o $O/k.o &
 /opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/bdpt_wavefront.hip -o $O/w.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $O/k.o $O/w.o lib/obj/bdpt_kernels_deep.o lib/obj/pt_kernels.o lib/obj/bdpt_capi.o lib/obj/scene.o lib/obj/wide_bvh.o lib/obj/toml_config.o lib/obj/exr_io.o -o lib/libbdpt_amd_$NAME.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $O/k.o $O/w.o lib/obj/bdpt_kernels_deep.o lib/obj/pt_kernels.o lib/obj/bdpt_capi.o lib/obj/math_check.o lib/obj/scene.o lib/obj/wide_bvh.o lib/obj/toml_config.o lib/obj/exr_io.o -o lib/libbdpt_amd_$NAME.so
 echo lib/libbdpt_amd_$NAME.so
