@@ -68,8 +68,12 @@ def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int, integrator: str 
     ref = os.path.join(REPO, "oracle", "_ref", "ref_bdpt")
     toml = os.path.join("/tmp", f"bench_{scene}_{os.getpid()}.toml")
     with open(toml, "w") as f:
-        f.write(variants.toml_text(scene, W, H, spp, rr) if integrator == "bdpt"
-                else variants.path_toml_text(scene, W, H, spp))
+        if integrator == "bdpt":
+            f.write(variants.toml_text(scene, W, H, spp, rr))
+        elif integrator == "path":
+            f.write(variants.path_toml_text(scene, W, H, spp))
+        else:
+            f.write(variants.direct_toml_text(scene, W, H, spp))
     # ~6 rows per thread: 10-20 s of wall time at the reference's ~18 us per caustic sample-thread
     stride = max(1, H // (6 * threads))
     if os.path.exists(ref):
@@ -83,7 +87,8 @@ def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int, integrator: str 
         import oracle as O
         sc = O.Scene(variants.obj_path(scene))
         cam = variants.SCENES[scene]["camera"]
-        p = O.make_params(cam, W, H, spp, rr) if integrator == "bdpt" else O.make_path_params(cam, W, H, spp)
+        p = (O.make_params(cam, W, H, spp, rr) if integrator == "bdpt" else
+             O.make_path_params(cam, W, H, spp) if integrator == "path" else O.make_direct_params(cam, W, H, spp))
         t = time.time()
         _, samples = sc.render(p, threads=threads, rows=list(range(0, H, stride)))
         secs = time.time() - t
@@ -105,9 +110,10 @@ def main() -> None:
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--rr-depth", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--integrator", choices=["bdpt", "path"], default="bdpt",
+    ap.add_argument("--integrator", choices=["bdpt", "path", "direct"], default="bdpt",
                     help="bdpt = the hot path (BASELINE metric); path = the reference's PathTracerIntegrator "
-                         "(path.h, cbox_bdpt_path.toml settings) on the same substrate, for comparison")
+                         "(path.h, cbox_bdpt_path.toml settings), direct = its DirectIntegrator (direct.h, MIS, "
+                         "1 emitter + 1 BSDF sample) on the same substrate, for comparison")
     ap.add_argument("--schedule", choices=["megakernel", "wavefront"], default="megakernel",
                     help="render schedule (BDPT_FLAG_WAVEFRONT for the shade/trace passes)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_caustic_512x512_256spp.json"),
@@ -131,6 +137,10 @@ def main() -> None:
     if args.integrator == "path":
         integ = bdpt_amd.PathTracerIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
                                               bdpt_amd.PathSettings(), device=local if world > 1 else 0)
+    elif args.integrator == "direct":
+        integ = bdpt_amd.DirectIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
+                                          bdpt_amd.DirectSettings(sampling_strategy="mis"),
+                                          device=local if world > 1 else 0)
     else:
         integ = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
                                         device=local if world > 1 else 0)
@@ -170,15 +180,19 @@ def main() -> None:
     local_samples = integ.stats()["samples"]
     avg_kernel_ms = sum(kernel_ms) / max(len(kernel_ms), 1)
 
-    if rank == 0 and args.integrator == "path":
-        out = {"metric": "Msamples/sec, PathTracerIntegrator (path.h, explicit, RR 0.95 past depth 5)",
+    if rank == 0 and args.integrator in ("path", "direct"):
+        metric = ("Msamples/sec, PathTracerIntegrator (path.h, explicit, RR 0.95 past depth 5)"
+                  if args.integrator == "path" else
+                  "Msamples/sec, DirectIntegrator (direct.h, MIS, 1 emitter + 1 BSDF sample)")
+        out = {"metric": metric,
                "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic camera samples",
-               "config": {"workload": f"path_{args.scene}_{W}x{H}_{spp}spp", "scene": SCENE_LABEL.get(args.scene),
+               "config": {"workload": f"{args.integrator}_{args.scene}_{W}x{H}_{spp}spp",
+                          "scene": SCENE_LABEL.get(args.scene),
                           "kernel_ms": round(avg_kernel_ms, 3)}}
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(args.scene, W, H, spp, rr, integrator="path")
+            out["cpu_baseline"] = cpu_baseline(args.scene, W, H, spp, rr, integrator=args.integrator)
         print(json.dumps(out), flush=True)
     elif rank == 0:
         # algorithmic bytes per sample from a counting pass (untimed, same seeds, smaller spp)
