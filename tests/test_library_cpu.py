@@ -106,3 +106,18 @@ def test_ingest_triangulation_matches_oracle_on_polygons(tmp_path):
     b = O.Scene(str(p)).dump()
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("gen", ["many_shapes_obj", "closed_box_obj"])
+def test_ingest_matches_oracle_on_generated_scenes(gen, tmp_path):
+    """The generated test scenes of the GPU suite (7008 shapes; the closed box
+    for deep rrDepth): product ingest == oracle ingest, and the shape count that
+    moves the shape -> emitter map out of the LDS tables."""
+    import oracle as O
+    obj = getattr(variants, gen)(str(tmp_path))
+    s = bdpt_amd.Scene(obj)
+    for x, y in zip(s.export(), O.Scene(obj).dump()):
+        assert np.array_equal(x, y)
+    info = s.info()
+    assert info["shapes"] == (7008 if gen == "many_shapes_obj" else 9)
+    assert info["emitters"] == 1
