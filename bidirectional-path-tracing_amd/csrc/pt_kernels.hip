@@ -213,6 +213,15 @@ enum : int {  // explicit-level steps between queries
 #ifndef PT_INLINE_ADVANCE
 #define PT_INLINE_ADVANCE 1  // pt_advance inlined: the lane state stays in registers (not scratch)
 #endif
+// The overlapped walk / advance schedule (as the BDPT megakernel's) runs for
+// the path tracer (+9 % on Caustic, 512²×64); the direct integrator's one-level
+// samples are faster without it (1439 vs 1334 Msamples/s).
+#ifndef PT_SHADE_READY
+#define PT_SHADE_READY 56
+#endif
+#ifndef PT_TRAV_SPLIT
+#define PT_TRAV_SPLIT 8
+#endif
 #ifndef PT_WAVES_PER_EU
 #define PT_WAVES_PER_EU 4  // 128 VGPRs, 4 blocks of 256 lanes per CU
 #endif
@@ -589,7 +598,7 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
     }
 }
 
-template <bool COUNT>
+template <bool COUNT, bool OVERLAP>
 __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const PtParams* __restrict__ pp) {
     const PtParams& P = *pp;
     __shared__ uint2 stack_mem[kLdsStack * 256];
@@ -606,6 +615,12 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
     L.rng.stride = P.nslots;
     const uint64_t total = P.fr.total_samples;
     bool exhausted = false;
+    const TravScene tsc = trav_scene(P.sc);
+    bool tracing = false, has_res = false;
+    TravState ts{};
+    RayInv ri{};
+    int res = -1;
+    float rt = 0.f, ru = 0.f, rv = 0.f;
     for (;;) {
         if (!exhausted) {  // refill idle lanes: one atomic per wave
             const uint64_t idle = __ballot(!L.busy);
@@ -633,7 +648,45 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
             if (exhausted) break;
             continue;
         }
-        if (L.busy) {
+        if constexpr (OVERLAP) {
+        // The BDPT megakernel's overlapped schedule: a lane keeps walking its
+        // query across iterations; lanes with a finished query wait until
+        // PT_SHADE_READY of the wave have one, then advance together.
+        if (L.busy && !tracing && !has_res) {
+            if (COUNT) cnt.c[0]++;
+            ri = ray_inv(L.ray);
+            if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root (bvh.h:277, :287)
+                res = -1, rt = L.ray.max_t, ru = rv = 0.f;
+                has_res = true;
+            } else if (!ri.fast) {
+                const TravResult q = traverse_binary<COUNT, Stack>(P.sc, L.ray, false, true, stk);
+                if (COUNT) cnt.c[2] += q.nodes, cnt.c[3] += q.tris, cnt.c[15] += q.exact;
+                res = q.best, rt = q.t, ru = q.u, rv = q.v;
+                has_res = true;
+            } else {
+                ts = trav_begin(tsc, L.ray);
+                tracing = true;
+            }
+        }
+        for (;;) {
+            const uint64_t tr = __ballot(tracing);
+            if (!tr) break;
+            if (__popcll(__ballot(has_res)) >= PT_SHADE_READY) break;
+            const bool at_leaf = (ts.link & kLeafBit) != 0;
+            const uint64_t lv = __ballot(tracing && at_leaf);
+            const bool do_leaf = __popcll(lv) * 4 >= __popcll(tr & ~lv) * PT_TRAV_SPLIT;
+            if (tracing && at_leaf == do_leaf && trav_step<COUNT>(tsc, L.ray, ri, false, ts, stk, cnt)) {
+                res = ts.best, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;
+                tracing = false;
+                has_res = true;
+            }
+        }
+        if (has_res) {
+            has_res = false;
+            pt_resolve<COUNT>(L, res, rt, ru, rv, P, slot, cnt);
+            if (COUNT && !L.busy) cnt.c[7] += L.rng.m.n;
+        }
+        } else if (L.busy) {
             if (COUNT) cnt.c[0]++;
             float t = 0.f, u = 0.f, v = 0.f;
             const int res = traverse<false, COUNT>(P.sc, L.ray, false, stk, t, u, v, cnt);
@@ -653,7 +706,7 @@ int pt_lds_stack() { return dev::kLdsStack; }
 
 int pt_blocks_per_cu(size_t dyn_lds) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pt_frame_kernel<false>, 256, dyn_lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pt_frame_kernel<false, true>, 256, dyn_lds) != hipSuccess ||
         n <= 0)
         n = 1;
     return n;
@@ -679,8 +732,11 @@ hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int
     if (e != hipSuccess) return e;
     const dev::PtParams* kp = static_cast<const dev::PtParams*>(dparams);
     const size_t lds = 4 * static_cast<size_t>(sc.lds_words);
-    if (fr.flags & 1u) hipLaunchKernelGGL((dev::pt_frame_kernel<true>), dim3(grid), dim3(256), lds, stream, kp);
-    else hipLaunchKernelGGL((dev::pt_frame_kernel<false>), dim3(grid), dim3(256), lds, stream, kp);
+    const bool count = (fr.flags & 1u) != 0, overlap = host.ps.direct == 0;
+    if (count && overlap) hipLaunchKernelGGL((dev::pt_frame_kernel<true, true>), dim3(grid), dim3(256), lds, stream, kp);
+    else if (count) hipLaunchKernelGGL((dev::pt_frame_kernel<true, false>), dim3(grid), dim3(256), lds, stream, kp);
+    else if (overlap) hipLaunchKernelGGL((dev::pt_frame_kernel<false, true>), dim3(grid), dim3(256), lds, stream, kp);
+    else hipLaunchKernelGGL((dev::pt_frame_kernel<false, false>), dim3(grid), dim3(256), lds, stream, kp);
     return hipGetLastError();
 }
 
