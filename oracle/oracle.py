@@ -38,6 +38,7 @@ class Params(ctypes.Structure):
         ("di_strategy", ctypes.c_int),  # DirectIntegrator samplingStrategy (DIRECT_STRATEGIES)
         ("di_emitter_samples", ctypes.c_int),
         ("di_bsdf_samples", ctypes.c_int),
+        ("seed_base", ctypes.c_uint32),
     ]
 
 
@@ -116,6 +117,7 @@ def make_params(cam: dict, width: int, height: int, spp: int, rr_depth: int, str
     p.fov = float(cam["fov"])
     p.width, p.height, p.spp, p.rr_depth = width, height, spp, rr_depth
     p.strategy = strategy
+    p.seed_base = 260450963  # the reference's Sampler seed (renderer.cpp:155)
     return p
 
 

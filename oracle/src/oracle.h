@@ -37,6 +37,9 @@ typedef struct {
     /* integrator 2: DirectIntegrator (direct.h), samplingStrategy 1 area, 2 solidAngle,
      * 3 cosineHemisphere, 4 bsdf, 5 mis (main.cpp:88-92) */
     int di_strategy, di_emitter_samples, di_bsdf_samples;
+    /* per-(pixel, sample) seeds are seed_base + pixel*spp + k; the reference's
+     * Sampler seed 260450963 (renderer.cpp:155) unless a test varies it */
+    uint32_t seed_base;
 } tro_params;
 
 /* Loads an OBJ (+ MTL) exactly as Scene::load does (reference

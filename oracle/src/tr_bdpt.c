@@ -1160,8 +1160,8 @@ static ray_t camera_ray(const ctx_t* c, const camdrv_t* cd, int pixel, tr_sample
     return r;
 }
 
-static inline uint32_t seed_for(int pixel, int spp, int k) {
-    return 260450963u + (uint32_t)pixel * (uint32_t)spp + (uint32_t)k;
+static inline uint32_t seed_for(uint32_t base, int pixel, int spp, int k) {
+    return base + (uint32_t)pixel * (uint32_t)spp + (uint32_t)k;
 }
 
 int64_t tro_render(const tro_scene* s, const tro_params* p, float* fb, int row_begin, int row_end, int row_stride) {
@@ -1176,7 +1176,7 @@ int64_t tro_render(const tro_scene* s, const tro_params* p, float* fb, int row_b
             int pixel = row * p->width + j;
             v3 acc = V3(0, 0, 0);
             for (int k = 0; k < p->spp; k++) {
-                mt_seed(smp, seed_for(pixel, p->spp, k));
+                mt_seed(smp, seed_for(p->seed_base, pixel, p->spp, k));
                 ray_t ray = camera_ray(&c, &cd, pixel, smp);
                 acc = vadd(acc, integrator_render(&c, ray, smp));
                 n++;
@@ -1196,7 +1196,7 @@ void tro_sample(const tro_scene* s, const tro_params* p, int pixel, int k, float
     camdrv_t cd;
     setup(&c, &cd, s, p, fb);
     tr_sampler* smp = (tr_sampler*)malloc(sizeof(tr_sampler));
-    mt_seed(smp, seed_for(pixel, p->spp, k));
+    mt_seed(smp, seed_for(p->seed_base, pixel, p->spp, k));
     ray_t ray = camera_ray(&c, &cd, pixel, smp);
     v3 L = integrator_render(&c, ray, smp);
     Li[0] = L.x;
