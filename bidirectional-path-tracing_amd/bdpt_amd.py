@@ -124,6 +124,9 @@ def lib():
         L.bdpt_config_load_toml.argtypes = [ctypes.c_char_p, ctypes.POINTER(_Config)]
         L.bdpt_render_path.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_PathParams), vp, vp]
         L.bdpt_render_path_host.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_PathParams), vp]
+        for fn, pt in (("bdpt_render_path_sample", _PathParams), ("bdpt_render_direct_sample", _DirectParams)):
+            getattr(L, fn).argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(pt), f32p, ctypes.c_uint32,
+                                       ctypes.POINTER(i32), f32p]
         L.bdpt_render_direct.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_DirectParams), vp, vp]
         L.bdpt_render_direct_host.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_DirectParams), vp]
         L.bdpt_direct_strategy.restype = i32
@@ -396,8 +399,16 @@ class PathTracerIntegrator(BDPTIntegrator):
         super().__init__(scene, config, device)
         self.path = path or PathSettings()
 
-    def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:  # noqa: D102
-        raise BdptError("single-sample render(ray, sampler) is only exported for the BDPT integrator")
+    def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:
+        """PathTracerIntegrator::render(const Ray&, Sampler&): Li of one sample; the sampler advances."""
+        r = (ctypes.c_float * 8)(*ray.o, *ray.d, ray.min_t, ray.max_t)
+        draws = ctypes.c_int32(sampler.draws)
+        Li = (ctypes.c_float * 3)()
+        p, pp = self.params(), self.path.c()
+        _check(lib().bdpt_render_path_sample(self._h, ctypes.byref(p), ctypes.byref(pp), r, sampler.seed,
+                                             ctypes.byref(draws), Li))
+        sampler.draws = draws.value
+        return np.array(Li[:], np.float32)
 
     def render_frame(self, row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> np.ndarray:
         if self.rgb is None:
@@ -423,8 +434,16 @@ class DirectIntegrator(BDPTIntegrator):
         super().__init__(scene, config, device)
         self.direct = direct or DirectSettings(sampling_strategy="mis")
 
-    def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:  # noqa: D102
-        raise BdptError("single-sample render(ray, sampler) is only exported for the BDPT integrator")
+    def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:
+        """DirectIntegrator::render(const Ray&, Sampler&): Li of one sample; the sampler advances."""
+        r = (ctypes.c_float * 8)(*ray.o, *ray.d, ray.min_t, ray.max_t)
+        draws = ctypes.c_int32(sampler.draws)
+        Li = (ctypes.c_float * 3)()
+        p, d = self.params(), self.direct.c()
+        _check(lib().bdpt_render_direct_sample(self._h, ctypes.byref(p), ctypes.byref(d), r, sampler.seed,
+                                               ctypes.byref(draws), Li))
+        sampler.draws = draws.value
+        return np.array(Li[:], np.float32)
 
     def render_frame(self, row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> np.ndarray:
         if self.rgb is None:

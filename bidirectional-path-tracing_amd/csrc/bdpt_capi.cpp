@@ -50,6 +50,10 @@ hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int
                      unsigned long long* counters, int grid, hipStream_t stream, void* dparams);
 int frame_kernel_block();
 int light_vertex_fields();
+hipError_t launch_pt_sample(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8],
+                            float4* levels, uint32_t* ring, uint2* gstack, const dev::Ray& ray, uint32_t seed,
+                            uint32_t draws, float* out, unsigned long long* counters, hipStream_t stream,
+                            void* dparams);
 hipError_t launch_math_check(int32_t fn, const float* x, const float* y, float* out, int64_t n, hipStream_t st);
 }  // namespace bdpt
 
@@ -631,6 +635,57 @@ int bdpt_render_direct_host(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_
     HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return BDPT_OK;
+}
+
+// One PathTracerIntegrator / DirectIntegrator::render(ray, sampler) call
+// (settings: the launch_pt block; levels: level-stack depth it needs).
+static int render_pt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const int32_t settings[8], int levels,
+                            const float ray[8], uint32_t seed, int32_t* draws, float Li[3]) {
+    if (!c || !p || !ray || !draws || !Li) return fail(BDPT_ERR_INVALID, "null argument");
+    if (*draws < 0 || *draws > 226)
+        return fail(BDPT_ERR_UNSUPPORTED, "the sampler must enter with fewer than 227 draws");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = ensure_pt(c, levels))) return rc;
+    const dev::DevFrame fr = make_frame(p);
+    const dev::Ray r{dev::f3{ray[0], ray[1], ray[2]}, dev::f3{ray[3], ray[4], ray[5]}, ray[6], ray[7]};
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, c->stream));
+    HIP_TRY(launch_pt_sample(c->sc, fr, settings, c->pt_levels, c->pt_ring, c->gstack, r, seed,
+                             static_cast<uint32_t>(*draws), c->sample_out, c->counters, c->stream, c->pt_dparams));
+    float out[4];
+    unsigned long long ctr[2];
+    HIP_TRY(hipMemcpyAsync(out, c->sample_out, sizeof(out), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(ctr, c->counters, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (ctr[1] != 0) return fail(BDPT_ERR_UNSUPPORTED, "the sample outgrew the path tracer's level stack");
+    Li[0] = out[0], Li[1] = out[1], Li[2] = out[2];
+    uint32_t used;
+    std::memcpy(&used, &out[3], 4);
+    *draws = static_cast<int32_t>(used);
+    return BDPT_OK;
+}
+
+int bdpt_render_path_sample(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_params* path,
+                            const float ray[8], uint32_t seed, int32_t* draws, float Li[3]) {
+    if (!path) return fail(BDPT_ERR_INVALID, "null argument");
+    if (path->emitter_samples < 0 || path->bsdf_samples < 0) return fail(BDPT_ERR_INVALID, "negative sample counts");
+    const bool rr = path->is_explicit && path->max_depth == -1;
+    const int levels = rr ? kPtMaxLevels : std::max(path->max_depth, 0) + 2;
+    if (levels > kPtMaxLevels) return fail(BDPT_ERR_UNSUPPORTED, "maxDepth > 510 is not supported");
+    int32_t settings[8] = {path->is_explicit ? 1 : 0, path->max_depth, path->rr_depth, 0, path->emitter_samples,
+                           path->bsdf_samples, levels, 0};
+    std::memcpy(&settings[3], &path->rr_prob, 4);
+    return render_pt_sample(c, p, settings, levels, ray, seed, draws, Li);
+}
+
+int bdpt_render_direct_sample(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direct_params* d,
+                              const float ray[8], uint32_t seed, int32_t* draws, float Li[3]) {
+    if (!d) return fail(BDPT_ERR_INVALID, "null argument");
+    if (d->sampling_strategy < BDPT_DIRECT_AREA || d->sampling_strategy > BDPT_DIRECT_MIS)
+        return fail(BDPT_ERR_INVALID, "Error: wrong strategy");  // direct.h:460
+    if (d->emitter_samples < 0 || d->bsdf_samples < 0) return fail(BDPT_ERR_INVALID, "negative sample counts");
+    const int32_t settings[8] = {1, -1, 0, 0, d->emitter_samples, d->bsdf_samples, 1, d->sampling_strategy};
+    return render_pt_sample(c, p, settings, 1, ray, seed, draws, Li);
 }
 
 int bdpt_debug_math(int32_t device, int32_t fn, const float* x, const float* y, float* out, int64_t n) {

@@ -69,6 +69,7 @@ struct PtParams {
     unsigned long long* work;
     unsigned long long* counters;  // [0] closest rays (counting pass), [1] level-stack overflows,
                                    // [2] samples past 227 draws, [3] past 624 draws, [7] RNG draws (counting pass)
+    float* li_out;                 // single-sample launch: Li is written here instead of the framebuffer
 };
 
 enum : uint32_t {  // the query a lane waits on / the step it resumes at
@@ -137,7 +138,9 @@ __device__ __forceinline__ Ray pt_ray(f3 o, f3 d) {
 
 // Finishes the sample: rgb[p] += Li * (1 / spp) (renderer.cpp:202, one sample at a time).
 __device__ __forceinline__ void pt_finish(PtLane& L, const PtParams& P, f3 Li) {
-    if (Li.x != 0.f || Li.y != 0.f || Li.z != 0.f) {
+    if (P.li_out) {  // Integrator::render(ray, sampler) returns Li to its caller
+        P.li_out[0] = Li.x, P.li_out[1] = Li.y, P.li_out[2] = Li.z;
+    } else if (Li.x != 0.f || Li.y != 0.f || Li.z != 0.f) {
         const float inv_spp = 1.f / static_cast<float>(P.fr.spp);
         float* px = P.fb + 3 * static_cast<size_t>(L.pixel);
         atomicAdd(px + 0, Li.x * inv_spp);
@@ -697,6 +700,35 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
     if (COUNT) flush_counts(cnt, P.counters);
 }
 
+// One PathTracerIntegrator / DirectIntegrator::render(ray, sampler) call on one
+// lane (path.h:235-245, direct.h:449-462): the sampler is std::mt19937(seed)
+// after `draws` outputs (< 227). out = Li.xyz, draws after the call.
+__global__ __launch_bounds__(64) void pt_sample_kernel(const PtParams* __restrict__ pp, Ray ray, uint32_t seed,
+                                                       uint32_t draws, float* __restrict__ out) {
+    const PtParams& P = *pp;
+    __shared__ uint2 stack_mem[kLdsStack * 64];
+    scene_tables_to_lds(P.sc);
+    if (threadIdx.x != 0) return;
+    const Stack stk{stack_mem, 64, kLdsStack, P.gstack, 1, 0};
+    Counts cnt;
+    for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
+    PtLane L;
+    L.rng.ring = P.ring;
+    L.rng.stride = 1;
+    L.rng.seed = seed;
+    mt_seed_skip(L.rng.m, seed, draws);
+    L.pixel = 0;
+    L.ray = ray;
+    L.q = PQ_PRIMARY;
+    L.busy = true;
+    while (L.busy) {
+        float t = 0.f, u = 0.f, v = 0.f;
+        const int res = traverse<false, false>(P.sc, L.ray, false, stk, t, u, v, cnt);
+        pt_resolve<false>(L, res, t, u, v, P, 0, cnt);
+    }
+    out[3] = __uint_as_float(L.rng.m.n);
+}
+
 }  // namespace dev
 
 // ------------------------------------------------------------ host side
@@ -727,7 +759,7 @@ hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int
     host.ps.max_levels = settings[6];
     host.ps.direct = settings[7];
     host.fb = fb, host.levels = levels, host.ring = ring, host.gstack = gstack, host.nslots = nslots;
-    host.work = work, host.counters = counters;
+    host.work = work, host.counters = counters, host.li_out = nullptr;
     hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);
     if (e != hipSuccess) return e;
     const dev::PtParams* kp = static_cast<const dev::PtParams*>(dparams);
@@ -737,6 +769,31 @@ hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int
     else if (count) hipLaunchKernelGGL((dev::pt_frame_kernel<true, false>), dim3(grid), dim3(256), lds, stream, kp);
     else if (overlap) hipLaunchKernelGGL((dev::pt_frame_kernel<false, true>), dim3(grid), dim3(256), lds, stream, kp);
     else hipLaunchKernelGGL((dev::pt_frame_kernel<false, false>), dim3(grid), dim3(256), lds, stream, kp);
+    return hipGetLastError();
+}
+
+hipError_t launch_pt_sample(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8],
+                            float4* levels, uint32_t* ring, uint2* gstack, const dev::Ray& ray, uint32_t seed,
+                            uint32_t draws, float* out, unsigned long long* counters, hipStream_t stream,
+                            void* dparams) {
+    dev::PtParams host{};
+    host.sc = sc;
+    host.fr = fr;
+    host.ps.is_explicit = settings[0];
+    host.ps.max_depth = settings[1];
+    host.ps.rr_depth = settings[2];
+    std::memcpy(&host.ps.rr_prob, &settings[3], 4);
+    host.ps.emitter_samples = settings[4];
+    host.ps.bsdf_samples = settings[5];
+    host.ps.max_levels = settings[6];
+    host.ps.direct = settings[7];
+    host.fb = nullptr, host.levels = levels, host.ring = ring, host.gstack = gstack, host.nslots = 1;
+    host.work = nullptr, host.counters = counters, host.li_out = out;
+    hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    const dev::PtParams* kp = static_cast<const dev::PtParams*>(dparams);
+    hipLaunchKernelGGL(dev::pt_sample_kernel, dim3(1), dim3(64), 4 * static_cast<size_t>(sc.lds_words), stream, kp,
+                       ray, seed, draws, out);
     return hipGetLastError();
 }
 

@@ -173,6 +173,11 @@ int bdpt_render_path(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_
                      void* hip_stream);
 int bdpt_render_path_host(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_path_params* path,
                           float* fb_host);
+/* One PathTracerIntegrator::render(ray, sampler) call (path.h:235-245): ray = o.xyz
+ * d.xyz min_t max_t; the sampler is std::mt19937(sampler_seed) after *sampler_draws
+ * (< 227) draws, updated on return. Returns Li. Synchronous. */
+int bdpt_render_path_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_path_params* path,
+                            const float ray[8], uint32_t sampler_seed, int32_t* sampler_draws, float Li[3]);
 
 /* ---- the reference's direct-light integrator (src/integrators/direct.h) ---- */
 #define BDPT_DIRECT_AREA 1              /* samplingStrategy "area"             renderArea :143-195 */
@@ -195,6 +200,10 @@ int bdpt_render_direct(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdp
                        float* fb_device, void* hip_stream);
 int bdpt_render_direct_host(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_direct_params* direct,
                             float* fb_host);
+/* One DirectIntegrator::render(ray, sampler) call (direct.h:449-462), as
+ * bdpt_render_path_sample. */
+int bdpt_render_direct_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_direct_params* direct,
+                              const float ray[8], uint32_t sampler_seed, int32_t* sampler_draws, float Li[3]);
 /* samplingStrategy string -> BDPT_DIRECT_* (0 when unknown). */
 int32_t bdpt_direct_strategy(const char* name);
 

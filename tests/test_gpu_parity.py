@@ -159,20 +159,14 @@ def test_gpu_empty_shard_leaves_framebuffer_untouched():
     assert np.all(fb == 7.0)
 
 
-@pytest.mark.parametrize("pixel,k", [(0, 0), (2080, 3), (1000, 15), (4095, 7), (2500, 9)])
-def test_gpu_single_sample_api_matches_oracle(pixel, k):
-    """BDPTIntegrator.render(ray, sampler) == the reference's render() for one sample."""
-    W = H = 64
-    spp = 16
-    it = integrator("caustic", W, H, spp, 8)
-    p = O.make_params(variants.SCENES["caustic"]["camera"], W, H, spp, 8)
-    sc = O.Scene(variants.obj_path("caustic"))
-    Li_ref, splats_ref = sc.sample(p, pixel, k)
-    # rebuild the camera ray the driver would pass (renderer.cpp:184-192)
+def driver_ray(p, name, pixel, k):
+    """The camera ray and sampler the offline driver hands to render() for
+    sample k of `pixel` (renderer.cpp:162-192: jitter draws first when spp > 1)."""
+    W, spp = p.width, p.spp
     cam = O.camera(p)
     c2w = cam[16:32].reshape(4, 4)  # column-major: c2w[col][row]
     invW, invH, angle, aspect = cam[64:68]
-    rs = np.random.RandomState((O.REFERENCE_SEED if hasattr(O, "REFERENCE_SEED") else 260450963) + pixel * spp + k)
+    rs = np.random.RandomState(260450963 + pixel * spp + k)
     u = rs.randint(0, 2**32, size=2, dtype=np.uint32).astype(np.float32) / np.float32(2**32)
     j, i = pixel % W, pixel // W
     f32 = np.float32
@@ -185,7 +179,20 @@ def test_gpu_single_sample_api_matches_oracle(pixel, k):
     d = d * (f32(1) / np.sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]))
     sampler = bdpt_amd.Sampler.for_sample(pixel, spp, k)
     sampler.draws = 2
-    Li = it.render(bdpt_amd.Ray(tuple(variants.SCENES["caustic"]["camera"]["eye"]), tuple(d), 1.0, 1000.0), sampler)
+    return bdpt_amd.Ray(tuple(variants.SCENES[name]["camera"]["eye"]), tuple(d), 1.0, 1000.0), sampler
+
+
+@pytest.mark.parametrize("pixel,k", [(0, 0), (2080, 3), (1000, 15), (4095, 7), (2500, 9)])
+def test_gpu_single_sample_api_matches_oracle(pixel, k):
+    """BDPTIntegrator.render(ray, sampler) == the reference's render() for one sample."""
+    W = H = 64
+    spp = 16
+    it = integrator("caustic", W, H, spp, 8)
+    p = O.make_params(variants.SCENES["caustic"]["camera"], W, H, spp, 8)
+    sc = O.Scene(variants.obj_path("caustic"))
+    Li_ref, splats_ref = sc.sample(p, pixel, k)
+    ray, sampler = driver_ray(p, "caustic", pixel, k)
+    Li = it.render(ray, sampler)
     assert np.allclose(Li, Li_ref, rtol=1e-6, atol=0), (Li, Li_ref)
     assert rel_l2(it.rgb.reshape(-1), splats_ref).max() <= TOL
     assert sampler.draws > 2
@@ -473,3 +480,28 @@ def test_gpu_randomized_configs_match_oracle(seed):
     worst, exact, _ = report(fb, ref)
     assert worst <= TOL, (f"{name} {W}x{H}x{spp} rr={rr} strategy={strategy} rows {off}::{stride} base={base}: "
                           f"max per-pixel rel L2 {worst:.3g}")
+
+
+@pytest.mark.parametrize("integ", ["path", "path_mis", "direct_mis", "direct_area"])
+def test_gpu_single_sample_api_other_integrators(integ):
+    """PathTracerIntegrator / DirectIntegrator.render(ray, sampler) == the
+    reference's render() of one sample (oracle), over several pixels."""
+    name, W, H, spp = "caustic", 48, 48, 8
+    cam = variants.SCENES[name]["camera"]
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**cam), width=W, height=H, spp=spp)
+    if integ.startswith("path"):
+        ps = dict(emitter_samples=2, bsdf_samples=2) if integ == "path_mis" else {}
+        it = bdpt_amd.PathTracerIntegrator(scene(name), cfg, bdpt_amd.PathSettings(**ps))
+        p = O.make_path_params(cam, W, H, spp, **ps)
+    else:
+        st = integ.split("_")[1]
+        it = bdpt_amd.DirectIntegrator(scene(name), cfg, bdpt_amd.DirectSettings(sampling_strategy=st,
+                                                                                  emitter_samples=2))
+        p = O.make_direct_params(cam, W, H, spp, strategy=st, emitter_samples=2)
+    sc = O.Scene(variants.obj_path(name))
+    for pixel, k in [(0, 0), (1111, 3), (1200, 7), (2000, 5), (1500, 1), (700, 6)]:
+        Li_ref, _ = sc.sample(p, pixel, k)
+        ray, sampler = driver_ray(p, name, pixel, k)
+        Li = it.render(ray, sampler)
+        assert np.allclose(Li, Li_ref, rtol=1e-6, atol=0), (pixel, k, Li, Li_ref)
+        assert sampler.draws >= 2
