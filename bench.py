@@ -47,24 +47,65 @@ SCENE_LABEL = {
 METRIC = "Msamples/sec (whole node) at 256 spp, Cornell caustic 512², 1/2/4/8 GPUs"
 
 
-def algorithmic_bytes_per_sample(c: dict, samples: int) -> float:
-    """SURVEY.md §8(d) byte model on this build's data layout, evaluated on its
-    own counting pass (DESIGN.md "Roofline"): 112 B per 4-wide node visit (six
-    child-bound float4 + the link float4), 48 B per triangle test (v0, e1, e2),
-    96 B per shaded closest hit (v0 + the 80-byte shading record), 64 B per
-    light vertex written or read, 12 B per framebuffer add (camera splats and
-    the per-sample eye estimate)."""
-    b = (112 * c["interior_visits"] + 48 * c["tri_tests"] + 96 * c["closest_rays"]
-         + 64 * (c["light_verts"] + c["light_vert_reads"]) + 12 * (c["splats"] + samples))
+# SURVEY.md §8(d) byte model (the figure `roofline.achieved` is priced on):
+# 64 B per interior node visit, 36 B per triangle test (3 float3 vertices), 40 B
+# per closest hit (3 normals + matID for shading), 64 B per light vertex written
+# or read, 12 B per framebuffer add (camera splats + the per-sample eye estimate).
+SURVEY_BYTES = dict(node=64, tri=36, hit=40, vertex=64, fb=12)
+# This build's own layout: 112 B per 4-wide node visit (six child-bound float4 +
+# the link float4), 48 B per triangle test (v0, e1, e2), 96 B per shaded closest
+# hit (v0 + the 80-byte shading record); vertices and framebuffer as above.
+LAYOUT_BYTES = dict(node=112, tri=48, hit=96, vertex=64, fb=12)
+
+
+def algorithmic_bytes_per_sample(c: dict, samples: int, m: dict = SURVEY_BYTES) -> float:
+    """Bytes per camera sample under byte model `m`, evaluated on the build's own
+    counting pass (same seeds): counters interior_visits, tri_tests,
+    closest_rays, light_verts + light_vert_reads, splats (+1 eye add)."""
+    b = (m["node"] * c["interior_visits"] + m["tri"] * c["tri_tests"] + m["hit"] * c["closest_rays"]
+         + m["vertex"] * (c["light_verts"] + c["light_vert_reads"]) + m["fb"] * (c["splats"] + samples))
     return b / max(samples, 1)
 
 
-def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int, integrator: str = "bdpt") -> dict:
+# Reference CPU cost per camera sample and thread (measured on the GPU box's host,
+# round 1) — only sizes the bounded CPU sample.
+CPU_US_PER_SAMPLE = {"caustic": 18.0, "hardlight": 5.0, "hardlight_mirror": 9.0, "cbox_low": 9.0, "synth1m": 35.0}
+
+
+def host_cpus() -> dict:
+    """The host cores this job may use: the scheduler affinity set, capped by the
+    cgroup CPU quota (on the GPU box the job's share of a larger machine; nproc
+    there reports the whole machine), plus the machine's CPU count and model."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"usable": usable, "nproc": os.cpu_count(), "affinity": aff, "cgroup_quota": quota, "model": model}
+
+
+def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int, integrator: str = "bdpt",
+                 frame_out: str | None = None) -> dict:
     """The reference CPU path (oracle/_ref/ref_bdpt = the unmodified reference
     BDPT compiled from its sources) on a bounded sample of the same workload:
-    every `stride`-th row of the 512x512 image at the bench spp, std::thread over
-    the host's cores. Falls back to the C restatement (kind "port")."""
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    every `stride`-th row of the image at the bench spp, std::thread over every
+    host core this job may use. With `frame_out`, the reference's framebuffer of
+    that row shard is written there (for the in-run parity check). Falls back to
+    the C restatement (kind "port") when the reference binary is absent."""
+    cpus = host_cpus()
+    threads = cpus["usable"]
     ref = os.path.join(REPO, "oracle", "_ref", "ref_bdpt")
     toml = os.path.join("/tmp", f"bench_{scene}_{os.getpid()}.toml")
     with open(toml, "w") as f:
@@ -74,29 +115,57 @@ def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int, integrator: str 
             f.write(variants.path_toml_text(scene, W, H, spp))
         else:
             f.write(variants.direct_toml_text(scene, W, H, spp))
-    # ~6 rows per thread: 10-20 s of wall time at the reference's ~18 us per caustic sample-thread
-    stride = max(1, H // (6 * threads))
+    # about 15 s of wall time at the reference's per-sample cost on one thread
+    target_samples = 15.0 * threads / (CPU_US_PER_SAMPLE.get(scene, 20.0) * 1e-6)
+    stride = max(1, int(round(H * W * spp / max(target_samples, 1.0))))
+    stride = min(stride, H)
     if os.path.exists(ref):
         rr_arg = ["--rr", str(rr)] if integrator == "bdpt" else []
+        out_arg = ["--out", frame_out] if frame_out else []
         out = subprocess.run([ref, "render", toml, str(W), str(H), str(spp), *rr_arg, "--threads",
-                              str(threads), "--row-stride", str(stride)], capture_output=True, text=True,
+                              str(threads), "--row-stride", str(stride), *out_arg], capture_output=True, text=True,
                              check=True, timeout=900)
         r = json.loads(out.stdout.strip().splitlines()[-1])
         kind, val, secs, samples = "reference", r["msamples_per_s"], r["seconds"], r["samples"]
     else:
+        import numpy as np
         import oracle as O
         sc = O.Scene(variants.obj_path(scene))
         cam = variants.SCENES[scene]["camera"]
         p = (O.make_params(cam, W, H, spp, rr) if integrator == "bdpt" else
              O.make_path_params(cam, W, H, spp) if integrator == "path" else O.make_direct_params(cam, W, H, spp))
         t = time.time()
-        _, samples = sc.render(p, threads=threads, rows=list(range(0, H, stride)))
+        fbo, samples = sc.render(p, threads=threads, rows=list(range(0, H, stride)))
         secs = time.time() - t
         kind, val = "port", samples / secs * 1e-6
+        if frame_out:
+            np.asarray(fbo, np.float32).tofile(frame_out)
     os.unlink(toml)
     return {"value": round(val, 6), "unit": "Msamples/s", "cores": threads, "kind": kind,
-            "sample": f"{scene} {W}x{H}, {spp} spp, every {stride}th row ({samples} camera samples, "
-                      f"{secs:.1f} s wall, {threads} threads)"}
+            "sample": f"{scene} {W}x{H}, {spp} spp, every {stride}th row from row 0 ({samples} camera samples, "
+                      f"{secs:.1f} s wall, {threads} threads)",
+            "row_stride": stride, "host": cpus}
+
+
+def frame_parity(gpu, ref) -> dict:
+    """Per-pixel relative L2 ||g - r|| / max(||r||, 1e-8) (north star: <= 1e-4)."""
+    import numpy as np
+
+    g = np.asarray(gpu, np.float64).reshape(-1, 3)
+    r = np.asarray(ref, np.float64).reshape(-1, 3)
+    err = np.linalg.norm(g - r, axis=1) / np.maximum(np.linalg.norm(r, axis=1), 1e-8)
+    return {"max_rel_l2": float(err.max()), "frac_pixels_over_1e-4": float((err > 1e-4).mean()),
+            "image_rel_l2": float(np.linalg.norm(g - r) / max(np.linalg.norm(r), 1e-30)),
+            "pixels": int(len(err)), "nonzero_pixels": int((np.abs(r).sum(1) > 0).sum())}
+
+
+def stamped(path: str, build: str) -> dict | None:
+    """A committed profile summary, only if it was measured on this kernel build."""
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d if d.get("kernel_build") == build else None
 
 
 def main() -> None:
@@ -116,8 +185,11 @@ def main() -> None:
                          "1 emitter + 1 BSDF sample) on the same substrate, for comparison")
     ap.add_argument("--schedule", choices=["megakernel", "wavefront"], default="megakernel",
                     help="render schedule (BDPT_FLAG_WAVEFRONT for the shade/trace passes)")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_caustic_512x512_256spp.json"),
-                    help="measured HBM bytes per launch (rocprofv3 --pmc summary) for roofline.traffic")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the in-run parity check of the GPU row shard against the CPU reference frame")
+    ap.add_argument("--profiles", default=os.path.join(REPO, "profiles"),
+                    help="directory of kernel-build-stamped PMC summaries (pmc_<workload>.json, "
+                         "pmc_deep_<workload>.json) for roofline.traffic / limiter")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -155,7 +227,12 @@ def main() -> None:
     def step():
         fb.zero_()
         integ.render_device(fb.data_ptr(), stream, row_offset=row_offset, row_stride=row_stride, flags=sched_flags)
-        kernel_ms.append(integ.stats()["kernel_ms"])  # waits for the render kernel's end event
+        st = integ.stats()  # waits for the render kernel's end event
+        kernel_ms.append(st["kernel_ms"])
+        if args.integrator == "path" and st["counters"]["shadow_rays"]:
+            # counters[1] of bdpt_render_path: samples that outgrew the 512-level
+            # recursion stack, whose result is then not the reference's
+            raise RuntimeError(f"{st['counters']['shadow_rays']} path samples outgrew the level stack")
         bdpt_dist.reduce_framebuffer(fb, dst=0)
 
     for _ in range(args.warmup):
@@ -201,14 +278,40 @@ def main() -> None:
         cbuf = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
         cnt.render_device(cbuf.data_ptr(), stream, flags=bdpt_amd.FLAG_COUNT | sched_flags)
         cst = cnt.stats()
-        bps = algorithmic_bytes_per_sample(cst["counters"], cst["samples"])
-        achieved = bps * local_samples / (avg_kernel_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.pmc):
-            with open(args.pmc) as f:
-                pm = json.load(f)
-            if pm.get("config") == f"{args.scene}_{W}x{H}_{spp}spp":
-                traffic = pm.get("hbm_bytes_per_launch")
+        cts = cst["counters"]
+        bps = algorithmic_bytes_per_sample(cts, cst["samples"], SURVEY_BYTES)
+        bps_layout = algorithmic_bytes_per_sample(cts, cst["samples"], LAYOUT_BYTES)
+        kernel_s = avg_kernel_ms * 1e-3
+        achieved = bps * local_samples / kernel_s / 1e9
+        workload = f"{args.scene}_{W}x{H}_{spp}spp"
+        build = bdpt_amd.kernel_build_hash()
+        # measured memory-side traffic and issue counters of THIS kernel build
+        # (rocprofv3 --pmc passes, tools/profile_round.sh / tools/pmc_deep.sh)
+        pm = stamped(os.path.join(args.profiles, f"pmc_{workload}.json"), build)
+        deep = stamped(os.path.join(args.profiles, f"pmc_deep_{workload}.json"), build)
+        traffic = pm["hbm_bytes_per_launch"] * local_samples / pm["samples_per_launch"] if pm else None
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
+                "kernel": "bdpt_frame_kernel" if args.schedule == "megakernel"
+                else "bdpt_shade_kernel + bdpt_trace_kernel",
+                "kernel_build": build, "schedule": args.schedule, "kernel_ms": round(avg_kernel_ms, 3),
+                "samples_per_launch": local_samples,
+                "byte_model": "SURVEY.md 8(d): 64 B/node visit, 36 B/triangle test, 40 B/closest hit, "
+                              "64 B/light vertex written or read, 12 B/framebuffer add",
+                "bytes_per_sample": round(bps, 1),
+                "bytes_per_sample_layout_model": round(bps_layout, 1),
+                "achieved_layout_model": round(bps_layout * local_samples / kernel_s / 1e9, 2),
+                "counts_per_sample": {k: round(v / cst["samples"], 3) for k, v in cts.items()}}
+        if traffic is not None:
+            roof["dram_achieved"] = round(traffic / kernel_s / 1e9, 2)
+            roof["dram_frac"] = round(traffic / kernel_s / 1e9 / HBM_PEAK_GBPS, 5)
+            roof["traffic_over_algorithmic"] = round(traffic / (bps * local_samples), 4)
+            roof["traffic_source"] = pm.get("source")
+        if deep is not None:
+            roof["limiter"] = deep.get("limiter")
+            for k in ("active_lane_frac", "valu_issue_frac", "wait_frac", "valu_insts_per_sample"):
+                roof[k] = deep.get(k)
+            roof["issue_source"] = deep.get("source")
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -226,16 +329,26 @@ def main() -> None:
             "config": {"workload": f"{args.scene}_{W}x{H}_{spp}spp", "scene": SCENE_LABEL.get(args.scene, args.scene),
                        "width": W, "height": H, "spp": spp, "rr_depth": rr, "samples_per_step": samples_total,
                        "parallelism": f"{world}-way row-interleaved shards + RCCL sum-reduce"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
-                         "kernel": "bdpt_frame_kernel" if args.schedule == "megakernel"
-                         else "bdpt_shade_kernel + bdpt_trace_kernel",
-                         "schedule": args.schedule, "kernel_ms": round(avg_kernel_ms, 3),
-                         "bytes_per_sample": round(bps, 1),
-                         "counts_per_sample": {k: round(v / cst["samples"], 3) for k, v in cst["counters"].items()}},
+            "roofline": roof,
         }
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(args.scene, W, H, spp, rr)
+            ref_fb = None if args.no_parity else os.path.join("/tmp", f"bench_ref_fb_{os.getpid()}.f32")
+            cb = cpu_baseline(args.scene, W, H, spp, rr, frame_out=ref_fb)
+            out["cpu_baseline"] = {k: v for k, v in cb.items() if k != "row_stride"}
+            if ref_fb is not None:
+                import numpy as np
+
+                # the same row shard on the GPU, same seeds: framebuffer parity in this run
+                pbuf = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
+                integ.render_device(pbuf.data_ptr(), stream, row_offset=0, row_stride=cb["row_stride"],
+                                    flags=sched_flags)
+                torch.cuda.synchronize(dev)
+                ref = np.fromfile(ref_fb, np.float32)
+                os.unlink(ref_fb)
+                par = frame_parity(pbuf.cpu().numpy(), ref)
+                par.update({"rows": f"every {cb['row_stride']}th row from 0", "spp": spp,
+                            "reference": cb["kind"], "tolerance": 1e-4})
+                out["parity"] = par
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

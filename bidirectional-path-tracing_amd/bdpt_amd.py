@@ -88,6 +88,23 @@ class _Stats(ctypes.Structure):
                 ("counters", ctypes.c_int64 * len(COUNTER_NAMES))]  # BDPT_NUM_COUNTERS
 
 
+# Sources that make up the frame kernels' code objects: their hash stamps the
+# profiles (PMC passes) so bench.py only reuses a measurement of the same kernel.
+KERNEL_SOURCES = ("csrc/bdpt_kernels.hip", "csrc/bdpt_path.hpp", "csrc/bdpt_device.hpp", "csrc/device_math.hpp",
+                  "csrc/bdpt_types.h", "Makefile")
+
+
+def kernel_build_hash() -> str:
+    """sha256[:16] over the frame kernel's sources and build flags."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(HERE, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def build(force: bool = False) -> str:
     """Compiles lib/libbdpt_amd.so in-tree with hipcc for gfx950."""
     if force or not os.path.exists(LIB_PATH):

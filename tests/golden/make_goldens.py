@@ -76,6 +76,15 @@ DIRECT_FRAMEBUFFERS = {
                                                                          bsdf_samples=1)),
 }
 
+# BASELINE configs[3] / [4] at their full size: the reference renders a two-row
+# shard (8 threads); the fixture keeps the shard's own rows (eye estimates plus the
+# splats that land on them) and block sums of the whole frame (every splat).
+# name: (scene, W, H, spp, rrDepth, row_offset, row_stride, block)
+LARGE_FRAMEBUFFERS = {
+    "L1_caustic_1024x1024_spp1024_rows2": ("caustic", 1024, 1024, 1024, 8, 300, 512, 32),
+    "L2_synth1m_2048x2048_spp512_rows2": ("synth1m", 2048, 2048, 512, 8, 700, 1024, 64),
+}
+
 SCENE_DUMPS = {"cbox_low": (64, 64), "caustic": (512, 512), "hardlight": (512, 512), "hardlight_mirror": (512, 512),
                "synth1m": (64, 64)}
 
@@ -102,7 +111,7 @@ def main() -> None:
         "framebuffers": dict(old.get("framebuffers", {})),
         "scenes": dict(old.get("scenes", {})),
     }
-    for sect in ("path_framebuffers", "direct_framebuffers"):
+    for sect in ("path_framebuffers", "direct_framebuffers", "large_framebuffers"):
         if sect in old:
             manifest[sect] = dict(old[sect])
     tmp = tempfile.mkdtemp()
@@ -164,6 +173,30 @@ def main() -> None:
                                                      mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
                                                      ref_seconds=info["seconds"])
         print(name, manifest["direct_framebuffers"][name]["sha256"][:16], info)
+    for name, (scene, W, H, spp, rr, off, stride, blk) in LARGE_FRAMEBUFFERS.items():
+        if only and name not in only:
+            continue
+        toml = os.path.join(tmp, name + ".toml")
+        with open(toml, "w") as f:
+            f.write(variants.toml_text(scene, W, H, spp, rr))
+        out = os.path.join(tmp, name + ".f32")
+        r = subprocess.run([REF, "render", toml, str(W), str(H), str(spp), "--rr", str(rr), "--out", out,
+                            "--row-offset", str(off), "--row-stride", str(stride), "--threads", "8"],
+                           capture_output=True, text=True, check=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        fb = np.fromfile(out, np.float32).reshape(H, W, 3)
+        rows = list(range(off, H, stride))
+        blocks = fb.astype(np.float64).reshape(H // blk, blk, W // blk, blk, 3).sum(axis=(1, 3))
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), rows=np.array(rows, np.int32), fb_rows=fb[rows],
+                            blocks=blocks)
+        manifest.setdefault("large_framebuffers", dict(old.get("large_framebuffers", {})))
+        manifest["large_framebuffers"][name] = dict(scene=scene, width=W, height=H, spp=spp, rr_depth=rr,
+                                                    row_offset=off, row_stride=stride, block=blk,
+                                                    samples=info["samples"], threads=8,
+                                                    sha256_rows=sha(fb[rows].tobytes()),
+                                                    frame_sum=[float(x) for x in blocks.sum((0, 1))],
+                                                    ref_seconds=info["seconds"])
+        print(name, info)
     for scene, (W, H) in SCENE_DUMPS.items():
         if only and scene not in only:
             continue

@@ -1,24 +1,40 @@
 #!/bin/bash
-# Round profile of the bench workload (run on the GPU box from the repo root):
+# Round profile of a bench workload (run on the GPU box from the repo root):
 #   1. rocprofv3 --kernel-trace --stats of bench.py (kernel time per launch)
 #   2. --pmc FETCH_SIZE pass, 3. --pmc WRITE_SIZE pass (separate: TCC counter budget)
-#   -> gpurun_out/round/{kt,fetch,write}, profiles/pmc_caustic_512x512_256spp.json
-# usage: tools/profile_round.sh TAG [bench args...]
+#   4. issue / latency counter groups, one pass each (per-block limits of MI355X_MICROARCH.md)
+#   -> gpurun_out/prof_TAG/..., profiles/pmc_<workload>.json, profiles/pmc_deep_<workload>.json
+#      (both stamped with the kernel build hash; bench.py uses them only for that build)
+# usage: tools/profile_round.sh TAG SCENE W H SPP
 set -e
 cd "$(dirname "$0")/.."
-TAG=$1; shift
+TAG=$1 SCENE=${2:-caustic} W=${3:-512} H=${4:-512} SPP=${5:-256}
 R=$PWD
+WL=${SCENE}_${W}x${H}_${SPP}spp
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 $R/bench.py --no-cpu $*"
+B="python3 $R/bench.py --no-cpu --scene $SCENE --width $W --height $H --spp $SPP"
+K="bdpt_frame_kernel<false, false>"
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $B --steps 2 --warmup 1 > $OUT/kt.log 2>&1
-timeout -k 10 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- $B --steps 1 --warmup 0 > $OUT/fetch.log 2>&1
-timeout -k 10 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- $B --steps 1 --warmup 0 > $OUT/write.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $B --steps 2 --warmup 1 > $OUT/kt.log 2>&1
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- $B --steps 1 --warmup 0 > $OUT/fetch.log 2>&1
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- $B --steps 1 --warmup 0 > $OUT/write.log 2>&1
+i=0
+while read -r grp; do
+  i=$((i + 1))
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $grp -d $OUT/deep/p$i -o p$i --output-format csv -- $B --steps 1 --warmup 0 > $OUT/deep_p$i.log 2>&1
+done <<'GROUPS'
+SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM
+SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU
+GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum
+GROUPS
 cd $R
 find $OUT/kt -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
-python3 tools/pmc_traffic.py $OUT/fetch $OUT/write caustic_512x512_256spp "bdpt_frame_kernel<false, false>" \
-  $OUT/pmc_caustic_512x512_256spp.json
+SAMPLES=$((W * H * SPP))
+CUS=$(python3 -c "import torch; print(torch.cuda.get_device_properties(0).multi_processor_count)")
+python3 tools/pmc_traffic.py $OUT/fetch $OUT/write $WL "$K" $SAMPLES profiles/pmc_$WL.json
+python3 tools/pmc_deep_json.py $OUT/deep $WL "$K" $SAMPLES $CUS profiles/pmc_deep_$WL.json
+cp $OUT/kernel_stats.csv profiles/${TAG}_kernel_stats_$WL.csv
 cat $OUT/kernel_stats.csv
 tail -1 $OUT/kt.log
