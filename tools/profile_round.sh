@@ -3,8 +3,8 @@
 #   1. rocprofv3 --kernel-trace --stats of bench.py (kernel time per launch)
 #   2. --pmc FETCH_SIZE pass, 3. --pmc WRITE_SIZE pass (separate: TCC counter budget)
 #   4. issue / latency counter groups, one pass each (per-block limits of MI355X_MICROARCH.md)
-#   -> gpurun_out/prof_TAG/..., profiles/pmc_<workload>.json, profiles/pmc_deep_<workload>.json
-#      (both stamped with the kernel build hash; bench.py uses them only for that build)
+#   -> gpurun_out/prof_TAG/{kernel_stats.csv, pmc_<workload>.json, pmc_deep_<workload>.json}
+#      (stamped with the kernel build hash; bench.py uses them, copied to profiles/, only for that build)
 # usage: tools/profile_round.sh TAG SCENE W H SPP
 set -e
 cd "$(dirname "$0")/.."
@@ -33,8 +33,8 @@ cd $R
 find $OUT/kt -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 SAMPLES=$((W * H * SPP))
 CUS=$(python3 -c "import torch; print(torch.cuda.get_device_properties(0).multi_processor_count)")
-python3 tools/pmc_traffic.py $OUT/fetch $OUT/write $WL "$K" $SAMPLES profiles/pmc_$WL.json
-python3 tools/pmc_deep_json.py $OUT/deep $WL "$K" $SAMPLES $CUS profiles/pmc_deep_$WL.json
-cp $OUT/kernel_stats.csv profiles/${TAG}_kernel_stats_$WL.csv
+# written under gpurun_out (merged back); copy them into profiles/ to commit them
+python3 tools/pmc_traffic.py $OUT/fetch $OUT/write $WL "$K" $SAMPLES $OUT/pmc_$WL.json
+python3 tools/pmc_deep_json.py $OUT/deep $WL "$K" $SAMPLES $CUS $OUT/pmc_deep_$WL.json
 cat $OUT/kernel_stats.csv
 tail -1 $OUT/kt.log
