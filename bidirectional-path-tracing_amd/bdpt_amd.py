@@ -83,6 +83,24 @@ class _Config(ctypes.Structure):  # bdpt_config
                 ("path", _PathParams), ("direct", _DirectParams), ("sampling_strategy", ctypes.c_char * 32)]
 
 
+class _Splat(ctypes.Structure):  # bdpt_splat
+    _fields_ = [("pixel", ctypes.c_int32), ("rgb", ctypes.c_float * 3)]
+
+
+# bdpt_hit (AcceleratorBVH::intersect's SurfaceInteraction fields)
+HIT_DTYPE = np.dtype([("hit", np.int32), ("t", np.float32), ("u", np.float32), ("v", np.float32),
+                      ("shape_id", np.int32), ("prim_id", np.int32), ("mat_id", np.int32), ("p", np.float32, 3),
+                      ("ns", np.float32, 3), ("ng", np.float32, 3), ("wo", np.float32, 3), ("tri", np.int32)])
+
+
+def _af32(a, cols):
+    return np.ascontiguousarray(np.asarray(a, np.float32).reshape(-1, cols))
+
+
+def _ai32(a):
+    return np.ascontiguousarray(np.asarray(a, np.int32).reshape(-1))
+
+
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
                 ("counters", ctypes.c_int64 * len(COUNTER_NAMES))]  # BDPT_NUM_COUNTERS
@@ -136,6 +154,22 @@ def lib():
         L.bdpt_render_host.argtypes = [vp, ctypes.POINTER(_FrameParams), vp]
         L.bdpt_render_sample.argtypes = [vp, ctypes.POINTER(_FrameParams), f32p, ctypes.c_uint32,
                                          ctypes.POINTER(i32), f32p, vp]
+        L.bdpt_sampler_state.argtypes = [ctypes.c_uint32, ctypes.c_int64, vp]
+        L.bdpt_render_sample_mt.argtypes = [vp, ctypes.POINTER(_FrameParams), f32p, vp, f32p,
+                                            ctypes.POINTER(_Splat), i32, ctypes.POINTER(i32)]
+        L.bdpt_render_path_sample_mt.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_PathParams), f32p,
+                                                 vp, f32p]
+        L.bdpt_render_direct_sample_mt.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_DirectParams),
+                                                   f32p, vp, f32p]
+        i64 = ctypes.c_int64
+        L.bdpt_bsdf_eval.argtypes = [vp, i64, vp, vp, vp, vp]
+        L.bdpt_bsdf_pdf.argtypes = [vp, i64, vp, vp, vp, vp]
+        L.bdpt_bsdf_sample.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp]
+        L.bdpt_bsdf_type.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(i32)]
+        L.bdpt_intersect.argtypes = [vp, i64, vp, i32, vp]
+        L.bdpt_splat_to_image_plane.argtypes = [vp, ctypes.POINTER(_FrameParams), i64, vp, vp]
+        L.bdpt_debug_fresnel.argtypes = [i32, i64, vp, vp]
+        L.bdpt_debug_triangle.argtypes = [i32, i64, vp, vp, vp]
         L.bdpt_get_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
         L.bdpt_synchronize.argtypes = [vp]
         L.bdpt_config_load_toml.argtypes = [ctypes.c_char_p, ctypes.POINTER(_Config)]
@@ -285,16 +319,62 @@ class Ray:
     max_t: float = 3.402823466e38
 
 
+MT19937_WORDS = 625  # BDPT_MT19937_WORDS: _M_x[624], _M_p (libstdc++'s operator<< order)
+
+
+def _mt_twist(x: np.ndarray) -> None:
+    """mersenne_twister_engine::_M_gen_rand (libstdc++ random.tcc) on x[0:624] in place."""
+    up, lo, a = np.uint32(0x80000000), np.uint32(0x7FFFFFFF), np.uint32(0x9908B0DF)
+    for k in range(624):
+        y = (x[k] & up) | (x[(k + 1) % 624] & lo)
+        x[k] = x[(k + 397) % 624] ^ (y >> np.uint32(1)) ^ (a if y & np.uint32(1) else np.uint32(0))
+
+
 class Sampler:
-    """std::mt19937(seed) plus the number of floats already drawn."""
+    """The reference's Sampler (src/core/math.h:63-76): a std::mt19937 and a
+    uniform_real_distribution<float>. `state` is the engine as libstdc++ streams
+    it (_M_x[624], then the position _M_p); the single-sample renders take and
+    advance it exactly as the reference does."""
 
     def __init__(self, seed: int):
-        self.seed = int(seed) & 0xFFFFFFFF
-        self.draws = 0
+        rs = np.random.RandomState(int(seed) & 0xFFFFFFFF)  # init_genrand == std::mt19937(seed)
+        key, pos = rs.get_state()[1:3]
+        self.state = np.concatenate([key.astype(np.uint32), [np.uint32(pos)]]).astype(np.uint32)
+
+    @staticmethod
+    def from_state(state) -> "Sampler":
+        s = Sampler(0)
+        st = np.ascontiguousarray(state, np.uint32).reshape(-1)
+        if st.size != MT19937_WORDS or st[-1] > 624:
+            raise ValueError("a std::mt19937 state is 624 words and a position <= 624")
+        s.state = st.copy()
+        return s
 
     @staticmethod
     def for_sample(pixel: int, spp: int, k: int, base: int = REFERENCE_SEED) -> "Sampler":
         return Sampler((base + pixel * spp + k) & 0xFFFFFFFF)
+
+    def next_u32(self) -> int:
+        x = self.state
+        if x[624] >= 624:
+            _mt_twist(x)
+            x[624] = 0
+        y = int(x[int(x[624])])
+        x[624] += 1
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9D2C5680
+        y ^= (y << 15) & 0xEFC60000
+        y ^= y >> 18
+        return y & 0xFFFFFFFF
+
+    def next(self) -> float:
+        """Sampler::next: generate_canonical<float, 24> (random.tcc:3348-3380)."""
+        f = np.float32(self.next_u32()) / np.float32(4294967296.0)
+        return float(f) if f < 1.0 else float(np.float32(0.99999994))
+
+    def next2D(self) -> tuple:
+        x = self.next()
+        return x, self.next()
 
 
 class Scene:
@@ -313,6 +393,13 @@ class Scene:
         i = _SceneInfo()
         _check(lib().bdpt_scene_get_info(self._h, ctypes.byref(i)))
         return {n: getattr(i, n) for n, _ in _SceneInfo._fields_}
+
+    def bsdf_type(self, mat: int) -> tuple:
+        """(BSDF::getType() flags, kind) of material `mat` (core.h:311; kind 1 diffuse,
+        2 mirror, 3 glass, 4 mixture, 5 phong, 0 null)."""
+        t, k = ctypes.c_uint32(0), ctypes.c_int32(0)
+        _check(lib().bdpt_bsdf_type(self._h, mat, ctypes.byref(t), ctypes.byref(k)))
+        return t.value, k.value
 
     def export(self):
         """(tri_f32[n,18], tri_i32[n,3], node_f32[m,6], node_u32[m,3]) in the reference's dump layout."""
@@ -366,18 +453,68 @@ class BDPTIntegrator:
         return p
 
     def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:
-        """Integrator::render(const Ray&, Sampler&): Li of one camera sample;
-        its light-path splats are added to self.rgb; the sampler advances."""
+        """Integrator::render(const Ray&, Sampler&) (bdpt.h:219-241): Li of one
+        camera sample; its light-path splats are added to self.rgb in order; the
+        sampler's std::mt19937 state advances as the reference advances it."""
         if self.rgb is None:
             self.init()
+        Li, splats = self.render_sample(ray, sampler)
+        rgb = self.rgb.reshape(-1, 3)
+        for px, v in splats:
+            rgb[px] += v
+        return Li
+
+    def render_sample(self, ray: Ray, sampler: Sampler):
+        """bdpt_render_sample_mt: (Li, [(pixel, rgb float32[3]), ...]) of one sample."""
         r = (ctypes.c_float * 8)(*ray.o, *ray.d, ray.min_t, ray.max_t)
-        draws = ctypes.c_int32(sampler.draws)
+        cap = max(self.config.rr_depth, 1)
+        sp = (_Splat * cap)()
+        n = ctypes.c_int32(0)
         Li = (ctypes.c_float * 3)()
         p = self.params()
-        _check(lib().bdpt_render_sample(self._h, ctypes.byref(p), r, sampler.seed, ctypes.byref(draws), Li,
-                                        self.rgb.ctypes.data))
-        sampler.draws = draws.value
-        return np.array(Li[:], np.float32)
+        st = np.ascontiguousarray(sampler.state, np.uint32)
+        _check(lib().bdpt_render_sample_mt(self._h, ctypes.byref(p), r, st.ctypes.data, Li, sp, cap, ctypes.byref(n)))
+        sampler.state = st
+        return np.array(Li[:], np.float32), [(sp[k].pixel, np.array(sp[k].rgb[:], np.float32)) for k in range(n.value)]
+
+    # ---- the BSDF plugin contract and the path's building blocks (per-function entry points)
+    def bsdf_eval(self, mat, wo, wi) -> np.ndarray:
+        """BSDF::eval (core.h:308) of scene materials mat[k] on local directions: f * cos(wi), (n, 3)."""
+        m, o, i = _ai32(mat), _af32(wo, 3), _af32(wi, 3)
+        out = np.zeros((m.size, 3), np.float32)
+        _check(lib().bdpt_bsdf_eval(self._h, m.size, m.ctypes.data, o.ctypes.data, i.ctypes.data, out.ctypes.data))
+        return out
+
+    def bsdf_pdf(self, mat, wo, wi) -> np.ndarray:
+        """BSDF::pdf (core.h:309): the solid-angle pdf of wi, (n,)."""
+        m, o, i = _ai32(mat), _af32(wo, 3), _af32(wi, 3)
+        out = np.zeros(m.size, np.float32)
+        _check(lib().bdpt_bsdf_pdf(self._h, m.size, m.ctypes.data, o.ctypes.data, i.ctypes.data, out.ctypes.data))
+        return out
+
+    def bsdf_sample(self, mat, wo, u):
+        """BSDF::sample (core.h:310): (f * cos, wi, pdf) for samples u (n, 2)."""
+        m, o, uu = _ai32(mat), _af32(wo, 3), _af32(u, 2)
+        f, wi, pdf = np.zeros((m.size, 3), np.float32), np.zeros((m.size, 3), np.float32), np.zeros(m.size, np.float32)
+        _check(lib().bdpt_bsdf_sample(self._h, m.size, m.ctypes.data, o.ctypes.data, uu.ctypes.data, f.ctypes.data,
+                                      wi.ctypes.data, pdf.ctypes.data))
+        return f, wi, pdf
+
+    def intersect(self, rays, occlusion: bool = False) -> np.ndarray:
+        """AcceleratorBVH::intersect (accel.h:125-172) or the occlusion query of
+        visibilityQuery (bvh.h:259-352) on rays (n, 8): a structured bdpt_hit array."""
+        r = _af32(rays, 8)
+        out = np.zeros(r.shape[0], HIT_DTYPE)
+        _check(lib().bdpt_intersect(self._h, r.shape[0], r.ctypes.data, 1 if occlusion else 0, out.ctypes.data))
+        return out
+
+    def splat_to_image_plane(self, points) -> np.ndarray:
+        """BDPTIntegrator::splatToImagePlane (bdpt.h:485-496) of points (n, 3): int32 (n, 2)."""
+        q = _af32(points, 3)
+        out = np.zeros((q.shape[0], 2), np.int32)
+        p = self.params()
+        _check(lib().bdpt_splat_to_image_plane(self._h, ctypes.byref(p), q.shape[0], q.ctypes.data, out.ctypes.data))
+        return out
 
     def render_frame(self, row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> np.ndarray:
         """All pixels x spp of the (sharded) image into self.rgb (host copy)."""
@@ -409,22 +546,21 @@ class BDPTIntegrator:
 
 class PathTracerIntegrator(BDPTIntegrator):
     """The reference's PathTracerIntegrator (src/integrators/path.h) on the same
-    GPU substrate: render_frame / render_device as for BDPT (the single-sample
-    render(ray, sampler) entry is BDPT-only)."""
+    GPU substrate: render(ray, sampler), render_frame and render_device as for BDPT."""
 
     def __init__(self, scene: Scene, config: Config, path: PathSettings | None = None, device: int = 0):
         super().__init__(scene, config, device)
         self.path = path or PathSettings()
 
     def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:
-        """PathTracerIntegrator::render(const Ray&, Sampler&): Li of one sample; the sampler advances."""
+        """PathTracerIntegrator::render(const Ray&, Sampler&) (path.h:235-245): Li of
+        one sample; the sampler's std::mt19937 state advances."""
         r = (ctypes.c_float * 8)(*ray.o, *ray.d, ray.min_t, ray.max_t)
-        draws = ctypes.c_int32(sampler.draws)
         Li = (ctypes.c_float * 3)()
         p, pp = self.params(), self.path.c()
-        _check(lib().bdpt_render_path_sample(self._h, ctypes.byref(p), ctypes.byref(pp), r, sampler.seed,
-                                             ctypes.byref(draws), Li))
-        sampler.draws = draws.value
+        st = np.ascontiguousarray(sampler.state, np.uint32)
+        _check(lib().bdpt_render_path_sample_mt(self._h, ctypes.byref(p), ctypes.byref(pp), r, st.ctypes.data, Li))
+        sampler.state = st
         return np.array(Li[:], np.float32)
 
     def render_frame(self, row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> np.ndarray:
@@ -452,14 +588,14 @@ class DirectIntegrator(BDPTIntegrator):
         self.direct = direct or DirectSettings(sampling_strategy="mis")
 
     def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:
-        """DirectIntegrator::render(const Ray&, Sampler&): Li of one sample; the sampler advances."""
+        """DirectIntegrator::render(const Ray&, Sampler&) (direct.h:449-462): Li of one
+        sample; the sampler's std::mt19937 state advances."""
         r = (ctypes.c_float * 8)(*ray.o, *ray.d, ray.min_t, ray.max_t)
-        draws = ctypes.c_int32(sampler.draws)
         Li = (ctypes.c_float * 3)()
         p, d = self.params(), self.direct.c()
-        _check(lib().bdpt_render_direct_sample(self._h, ctypes.byref(p), ctypes.byref(d), r, sampler.seed,
-                                               ctypes.byref(draws), Li))
-        sampler.draws = draws.value
+        st = np.ascontiguousarray(sampler.state, np.uint32)
+        _check(lib().bdpt_render_direct_sample_mt(self._h, ctypes.byref(p), ctypes.byref(d), r, st.ctypes.data, Li))
+        sampler.state = st
         return np.array(Li[:], np.float32)
 
     def render_frame(self, row_offset: int = 0, row_stride: int = 1, flags: int = 0) -> np.ndarray:
@@ -485,4 +621,20 @@ def debug_math(fn: str, x: np.ndarray, y: np.ndarray | None = None, device: int 
     out = np.empty_like(x)
     _check(lib().bdpt_debug_math(device, code, x.ctypes.data, None if yy is None else yy.ctypes.data,
                                  out.ctypes.data, x.size))
+    return out
+
+
+def debug_fresnel(inp, device: int = 0) -> np.ndarray:
+    """GlassBSDF::FresnelDielectric (glass.h:40-53) on (n, 4) = (eta_i, eta_t, cos_i, cos_t)."""
+    x = _af32(inp, 4)
+    out = np.zeros(x.shape[0], np.float32)
+    _check(lib().bdpt_debug_fresnel(device, x.shape[0], x.ctypes.data, out.ctypes.data))
+    return out
+
+
+def debug_triangle(rays, verts, device: int = 0) -> np.ndarray:
+    """rayTriangleIntersect (core.h:379-400): (n, 4) = (hit, t, u, v) for rays (n, 8), verts (n, 9)."""
+    r, v = _af32(rays, 8), _af32(verts, 9)
+    out = np.zeros((r.shape[0], 4), np.float32)
+    _check(lib().bdpt_debug_triangle(device, r.shape[0], r.ctypes.data, v.ctypes.data, out.ctypes.data))
     return out

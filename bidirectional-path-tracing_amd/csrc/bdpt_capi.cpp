@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <random>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -22,8 +24,20 @@ hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float*
                         uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
                         hipStream_t stream, void* dparams);
 size_t frame_params_bytes();
-hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
-                         const dev::Ray& ray, uint32_t seed, uint32_t draws, float* out, hipStream_t stream);
+// sample_state.hip: the single-sample kernels (the caller's std::mt19937 state at sc.mt_ring)
+hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* splats, float* lvbuf, uint2* gstack,
+                         const dev::Ray& ray, float* out, hipStream_t stream);
+hipError_t launch_pt_sample(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8],
+                            float4* levels, uint32_t* ring, uint2* gstack, const dev::Ray& ray, float* out,
+                            unsigned long long* counters, hipStream_t stream, void* dparams);
+// kat_kernels.hip: per-function entry points
+hipError_t launch_bsdf_kat(const dev::DevScene& sc, int mode, int64_t n, const int32_t* mat, const float* wo,
+                           const float* x, float* out, hipStream_t st);
+hipError_t launch_fresnel_kat(int64_t n, const float* in, float* out, hipStream_t st);
+hipError_t launch_triangle_kat(int64_t n, const float* rays, const float* verts, float* out, hipStream_t st);
+hipError_t launch_intersect_kat(const dev::DevScene& sc, int64_t n, int occlusion, const float* rays, uint2* gstack,
+                                uint32_t nslots, float* out, hipStream_t st);
+hipError_t launch_splat_kat(const dev::DevFrame& fr, int64_t n, const float* p, int32_t* xy, hipStream_t st);
 int frame_kernel_lds_stack();
 size_t wf_params_bytes();
 int wf_lane_chunks();
@@ -50,10 +64,6 @@ hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int
                      unsigned long long* counters, int grid, hipStream_t stream, void* dparams);
 int frame_kernel_block();
 int light_vertex_fields();
-hipError_t launch_pt_sample(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8],
-                            float4* levels, uint32_t* ring, uint2* gstack, const dev::Ray& ray, uint32_t seed,
-                            uint32_t draws, float* out, unsigned long long* counters, hipStream_t stream,
-                            void* dparams);
 hipError_t launch_math_check(int32_t fn, const float* x, const float* y, float* out, int64_t n, hipStream_t st);
 }  // namespace bdpt
 
@@ -79,6 +89,21 @@ constexpr int kMaxRrDepth = 1024;  // beyond 28 the megakernel continues MT19937
 
 // Error reporting shared with the other C-ABI translation units (exr_io.cpp, toml_config.cpp).
 int bdpt::set_error(int code, const std::string& msg) { return fail(code, msg); }
+
+// The state of std::mt19937(seed) after `draws` outputs, as libstdc++'s
+// operator<< writes it: _M_x[0..623], then _M_p.
+static void mt19937_state(uint32_t seed, int64_t draws, uint32_t st[BDPT_MT19937_WORDS]) {
+    std::mt19937 g(seed);
+    g.discard(static_cast<unsigned long long>(draws));
+    std::ostringstream os;
+    os << g;
+    std::istringstream is(os.str());
+    for (int i = 0; i < BDPT_MT19937_WORDS; i++) {
+        unsigned long long v = 0;
+        is >> v;
+        st[i] = static_cast<uint32_t>(v);
+    }
+}
 
 struct bdpt_scene {
     HostScene host;
@@ -131,10 +156,33 @@ struct bdpt_ctx {
     uint32_t* pt_ring = nullptr;
     uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28)
     void* pt_dparams = nullptr;
+    // single-sample calls: the caller's std::mt19937 state and the splat list
+    uint32_t* mt_state = nullptr;  // BDPT_MT19937_WORDS
+    float* splat_list = nullptr;   // header (count, capacity) + capacity (pixel, r, g, b) records
+    int32_t splat_cap = 0;
+    // cross-stream ordering of the context's buffers: the last call's stream and
+    // an event recorded on it after that call's work
+    hipEvent_t last_use = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool used = false;
     // stats of the last render
     bool pending_timing = false;
     bdpt_stats stats{};
 };
+
+// Calls on one context are ordered even when they use different streams: a
+// call first makes its stream wait for the previous call's work (an event
+// recorded at that call's end), since all calls share the context's buffers.
+static int begin_use(bdpt_ctx* c, hipStream_t st) {
+    if (c->used && c->last_stream != st) HIP_TRY(hipStreamWaitEvent(st, c->last_use, 0));
+    return BDPT_OK;
+}
+static int end_use(bdpt_ctx* c, hipStream_t st) {
+    HIP_TRY(hipEventRecord(c->last_use, st));
+    c->last_stream = st;
+    c->used = true;
+    return BDPT_OK;
+}
 
 extern "C" {
 
@@ -245,11 +293,13 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
                     static_cast<void*>(c->sstack), c->wf_dparams,
                     static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams,
                     static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
-                    static_cast<void*>(c->mt_ring)})
+                    static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state),
+                    static_cast<void*>(c->splat_list)})
         if (p) (void)hipFree(p);
     if (c->host_ctr) (void)hipHostFree(c->host_ctr);
     for (hipEvent_t e : c->chunk_ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->last_use) (void)hipEventDestroy(c->last_use);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -271,6 +321,7 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&c->ev0));
     HIP_TRY(hipEventCreate(&c->ev1));
+    HIP_TRY(hipEventCreateWithFlags(&c->last_use, hipEventDisableTiming));
     const DeviceLayout& L = s->layout;
     void* p;
     int rc;
@@ -479,6 +530,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
         sc.mt_ring = c->mt_ring;
         sc.mt_ring_stride = c->nslots;
     }
+    if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
@@ -502,6 +554,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
         }
     }
     HIP_TRY(hipEventRecord(c->ev1, st));
+    if ((rc = end_use(c, st))) return rc;
     c->pending_timing = true;
     c->stats = bdpt_stats{};
     c->stats.samples = static_cast<int64_t>(fr.total_samples);
@@ -559,6 +612,7 @@ int bdpt_render_path(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_pa
     int32_t settings[8] = {path->is_explicit ? 1 : 0, path->max_depth, path->rr_depth, 0, path->emitter_samples,
                            path->bsdf_samples, levels, 0};
     std::memcpy(&settings[3], &path->rr_prob, 4);
+    if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
@@ -566,6 +620,7 @@ int bdpt_render_path(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_pa
         HIP_TRY(launch_pt(c->sc, fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
                           c->counters, c->pt_grid, st, c->pt_dparams));
     HIP_TRY(hipEventRecord(c->ev1, st));
+    if ((rc = end_use(c, st))) return rc;
     c->pending_timing = true;
     c->stats = bdpt_stats{};
     c->stats.samples = static_cast<int64_t>(fr.total_samples);
@@ -609,6 +664,7 @@ int bdpt_render_direct(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direc
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const dev::DevFrame fr = make_frame(p);
     const int32_t settings[8] = {1, -1, 0, 0, d->emitter_samples, d->bsdf_samples, 1, d->sampling_strategy};
+    if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
@@ -616,6 +672,7 @@ int bdpt_render_direct(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direc
         HIP_TRY(launch_pt(c->sc, fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
                           c->counters, c->pt_grid, st, c->pt_dparams));
     HIP_TRY(hipEventRecord(c->ev1, st));
+    if ((rc = end_use(c, st))) return rc;
     c->pending_timing = true;
     c->stats = bdpt_stats{};
     c->stats.samples = static_cast<int64_t>(fr.total_samples);
@@ -637,55 +694,124 @@ int bdpt_render_direct_host(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_
     return BDPT_OK;
 }
 
-// One PathTracerIntegrator / DirectIntegrator::render(ray, sampler) call
-// (settings: the launch_pt block; levels: level-stack depth it needs).
+static int ensure_sample_buffers(bdpt_ctx* c, int32_t splat_cap) {
+    if (!c->mt_state) HIP_TRY(hipMalloc(&c->mt_state, sizeof(uint32_t) * BDPT_MT19937_WORDS));
+    if (splat_cap > c->splat_cap) {
+        if (c->splat_list) HIP_TRY(hipFree(c->splat_list));
+        c->splat_list = nullptr;
+        HIP_TRY(hipMalloc(&c->splat_list, sizeof(float) * 4 * (static_cast<size_t>(splat_cap) + 1)));
+        c->splat_cap = splat_cap;
+    }
+    return BDPT_OK;
+}
+
+static int check_mt_state(const uint32_t* state) {
+    if (!state) return fail(BDPT_ERR_INVALID, "null sampler state");
+    if (state[BDPT_MT19937_WORDS - 1] > 624u) return fail(BDPT_ERR_INVALID, "sampler state position _M_p > 624");
+    return BDPT_OK;
+}
+
+// One PathTracerIntegrator / DirectIntegrator::render(ray, sampler) call with the
+// caller's std::mt19937 state (settings: the launch_pt block; levels: level-stack
+// depth it needs).
 static int render_pt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const int32_t settings[8], int levels,
-                            const float ray[8], uint32_t seed, int32_t* draws, float Li[3]) {
-    if (!c || !p || !ray || !draws || !Li) return fail(BDPT_ERR_INVALID, "null argument");
-    if (*draws < 0 || *draws > 226)
-        return fail(BDPT_ERR_UNSUPPORTED, "the sampler must enter with fewer than 227 draws");
-    HIP_TRY(hipSetDevice(c->device));
+                            const float ray[8], uint32_t* state, float Li[3], uint32_t* taken = nullptr) {
+    if (!c || !p || !ray || !Li) return fail(BDPT_ERR_INVALID, "null argument");
     int rc;
+    if ((rc = check_mt_state(state))) return rc;
+    HIP_TRY(hipSetDevice(c->device));
     if ((rc = ensure_pt(c, levels))) return rc;
+    if ((rc = ensure_sample_buffers(c, 1))) return rc;
+    if ((rc = begin_use(c, c->stream))) return rc;
     const dev::DevFrame fr = make_frame(p);
     const dev::Ray r{dev::f3{ray[0], ray[1], ray[2]}, dev::f3{ray[3], ray[4], ray[5]}, ray[6], ray[7]};
+    dev::DevScene sc = c->sc;
+    sc.mt_ring = c->mt_state;  // the sample kernel's generator state (mt_state_u32)
+    HIP_TRY(hipMemcpyAsync(c->mt_state, state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyHostToDevice,
+                           c->stream));
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, c->stream));
-    HIP_TRY(launch_pt_sample(c->sc, fr, settings, c->pt_levels, c->pt_ring, c->gstack, r, seed,
-                             static_cast<uint32_t>(*draws), c->sample_out, c->counters, c->stream, c->pt_dparams));
+    HIP_TRY(launch_pt_sample(sc, fr, settings, c->pt_levels, c->pt_ring, c->gstack, r, c->sample_out, c->counters,
+                             c->stream, c->pt_dparams));
     float out[4];
     unsigned long long ctr[2];
     HIP_TRY(hipMemcpyAsync(out, c->sample_out, sizeof(out), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(ctr, c->counters, sizeof(ctr), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(state, c->mt_state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyDeviceToHost,
+                           c->stream));
+    if ((rc = end_use(c, c->stream))) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (ctr[1] != 0) return fail(BDPT_ERR_UNSUPPORTED, "the sample outgrew the path tracer's level stack");
     Li[0] = out[0], Li[1] = out[1], Li[2] = out[2];
-    uint32_t used;
-    std::memcpy(&used, &out[3], 4);
-    *draws = static_cast<int32_t>(used);
+    if (taken) std::memcpy(taken, &out[3], 4);
+    return BDPT_OK;
+}
+
+static int path_sample_settings(const bdpt_path_params* path, int32_t settings[8], int& levels) {
+    if (!path) return fail(BDPT_ERR_INVALID, "null argument");
+    if (path->emitter_samples < 0 || path->bsdf_samples < 0) return fail(BDPT_ERR_INVALID, "negative sample counts");
+    const bool rr = path->is_explicit && path->max_depth == -1;
+    levels = rr ? kPtMaxLevels : std::max(path->max_depth, 0) + 2;
+    if (levels > kPtMaxLevels) return fail(BDPT_ERR_UNSUPPORTED, "maxDepth > 510 is not supported");
+    const int32_t s[8] = {path->is_explicit ? 1 : 0, path->max_depth, path->rr_depth, 0, path->emitter_samples,
+                          path->bsdf_samples, levels, 0};
+    std::memcpy(settings, s, sizeof(s));
+    std::memcpy(&settings[3], &path->rr_prob, 4);
+    return BDPT_OK;
+}
+
+static int direct_sample_settings(const bdpt_direct_params* d, int32_t settings[8]) {
+    if (!d) return fail(BDPT_ERR_INVALID, "null argument");
+    if (d->sampling_strategy < BDPT_DIRECT_AREA || d->sampling_strategy > BDPT_DIRECT_MIS)
+        return fail(BDPT_ERR_INVALID, "Error: wrong strategy");  // direct.h:460
+    if (d->emitter_samples < 0 || d->bsdf_samples < 0) return fail(BDPT_ERR_INVALID, "negative sample counts");
+    const int32_t s[8] = {1, -1, 0, 0, d->emitter_samples, d->bsdf_samples, 1, d->sampling_strategy};
+    std::memcpy(settings, s, sizeof(s));
+    return BDPT_OK;
+}
+
+int bdpt_render_path_sample_mt(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_params* path,
+                               const float ray[8], uint32_t state[BDPT_MT19937_WORDS], float Li[3]) {
+    int32_t settings[8];
+    int levels = 0, rc;
+    if ((rc = path_sample_settings(path, settings, levels))) return rc;
+    return render_pt_sample(c, p, settings, levels, ray, state, Li);
+}
+
+int bdpt_render_direct_sample_mt(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direct_params* d,
+                                 const float ray[8], uint32_t state[BDPT_MT19937_WORDS], float Li[3]) {
+    int32_t settings[8];
+    int rc;
+    if ((rc = direct_sample_settings(d, settings))) return rc;
+    return render_pt_sample(c, p, settings, 1, ray, state, Li);
+}
+
+// (seed, draws) sampler: std::mt19937(seed) advanced by *draws outputs.
+static int pt_sample_seeded(bdpt_ctx* c, const bdpt_frame_params* p, const int32_t settings[8], int levels,
+                            const float ray[8], uint32_t seed, int32_t* draws, float Li[3]) {
+    if (!draws) return fail(BDPT_ERR_INVALID, "null argument");
+    if (*draws < 0) return fail(BDPT_ERR_INVALID, "negative draw count");
+    uint32_t st[BDPT_MT19937_WORDS], used = 0;
+    mt19937_state(seed, *draws, st);
+    int rc;
+    if ((rc = render_pt_sample(c, p, settings, levels, ray, st, Li, &used))) return rc;
+    *draws += static_cast<int32_t>(used);
     return BDPT_OK;
 }
 
 int bdpt_render_path_sample(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_params* path,
                             const float ray[8], uint32_t seed, int32_t* draws, float Li[3]) {
-    if (!path) return fail(BDPT_ERR_INVALID, "null argument");
-    if (path->emitter_samples < 0 || path->bsdf_samples < 0) return fail(BDPT_ERR_INVALID, "negative sample counts");
-    const bool rr = path->is_explicit && path->max_depth == -1;
-    const int levels = rr ? kPtMaxLevels : std::max(path->max_depth, 0) + 2;
-    if (levels > kPtMaxLevels) return fail(BDPT_ERR_UNSUPPORTED, "maxDepth > 510 is not supported");
-    int32_t settings[8] = {path->is_explicit ? 1 : 0, path->max_depth, path->rr_depth, 0, path->emitter_samples,
-                           path->bsdf_samples, levels, 0};
-    std::memcpy(&settings[3], &path->rr_prob, 4);
-    return render_pt_sample(c, p, settings, levels, ray, seed, draws, Li);
+    int32_t settings[8];
+    int levels = 0, rc;
+    if ((rc = path_sample_settings(path, settings, levels))) return rc;
+    return pt_sample_seeded(c, p, settings, levels, ray, seed, draws, Li);
 }
 
 int bdpt_render_direct_sample(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direct_params* d,
                               const float ray[8], uint32_t seed, int32_t* draws, float Li[3]) {
-    if (!d) return fail(BDPT_ERR_INVALID, "null argument");
-    if (d->sampling_strategy < BDPT_DIRECT_AREA || d->sampling_strategy > BDPT_DIRECT_MIS)
-        return fail(BDPT_ERR_INVALID, "Error: wrong strategy");  // direct.h:460
-    if (d->emitter_samples < 0 || d->bsdf_samples < 0) return fail(BDPT_ERR_INVALID, "negative sample counts");
-    const int32_t settings[8] = {1, -1, 0, 0, d->emitter_samples, d->bsdf_samples, 1, d->sampling_strategy};
-    return render_pt_sample(c, p, settings, 1, ray, seed, draws, Li);
+    int32_t settings[8];
+    int rc;
+    if ((rc = direct_sample_settings(d, settings))) return rc;
+    return pt_sample_seeded(c, p, settings, 1, ray, seed, draws, Li);
 }
 
 int bdpt_debug_math(int32_t device, int32_t fn, const float* x, const float* y, float* out, int64_t n) {
@@ -758,30 +884,240 @@ int bdpt_render_host(bdpt_ctx* c, const bdpt_frame_params* p, float* fb_host) {
     return BDPT_OK;
 }
 
-int bdpt_render_sample(bdpt_ctx* c, const bdpt_frame_params* p, const float ray[8], uint32_t seed,
-                       int32_t* draws, float Li[3], float* fb_host) {
-    if (!c || !ray || !draws || !Li || !fb_host) return fail(BDPT_ERR_INVALID, "null argument");
+static int render_bdpt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const float ray[8], uint32_t* state,
+                              float Li[3], bdpt_splat* splats, int32_t capacity, int32_t* nsplats, uint32_t* taken) {
+    if (!c || !ray || !Li || !nsplats || (capacity > 0 && !splats) || capacity < 0)
+        return fail(BDPT_ERR_INVALID, "null argument");
     int rc = check_params(p);
     if (rc) return rc;
-    if (*draws < 0 || *draws + 10 + 8 * (p->rr_depth - 1) > 226)
-        return fail(BDPT_ERR_UNSUPPORTED, "sampler advanced beyond the lazy MT19937 window");
+    if ((rc = check_mt_state(state))) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t n = static_cast<size_t>(p->width) * p->height * 3;
-    if ((rc = ensure_tmp_fb(c, n))) return rc;
     if ((rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
-    HIP_TRY(hipMemcpyAsync(c->tmp_fb, fb_host, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    // a sample splats at most once per light vertex: rr_depth bounds the list
+    if ((rc = ensure_sample_buffers(c, std::max(p->rr_depth, 1)))) return rc;
+    if ((rc = begin_use(c, c->stream))) return rc;
     const dev::DevFrame fr = make_frame(p);
-    dev::Ray r{dev::f3{ray[0], ray[1], ray[2]}, dev::f3{ray[3], ray[4], ray[5]}, ray[6], ray[7]};
-    HIP_TRY(launch_sample(c->sc, fr, c->tmp_fb, c->lv, c->gstack, r, seed, static_cast<uint32_t>(*draws), c->sample_out, c->stream));
+    dev::DevScene sc = c->sc;
+    sc.mt_ring = c->mt_state;  // the sample kernel's generator state (mt_state_u32)
+    const dev::Ray r{dev::f3{ray[0], ray[1], ray[2]}, dev::f3{ray[3], ray[4], ray[5]}, ray[6], ray[7]};
+    const uint32_t hdr[4] = {0u, static_cast<uint32_t>(c->splat_cap), 0u, 0u};
+    HIP_TRY(hipMemcpyAsync(c->mt_state, state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(hipMemcpyAsync(c->splat_list, hdr, sizeof(hdr), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(launch_sample(sc, fr, c->splat_list, c->lv, c->gstack, r, c->sample_out, c->stream));
+    std::vector<float> list(4 * (static_cast<size_t>(c->splat_cap) + 1));
     float out[4];
     HIP_TRY(hipMemcpyAsync(out, c->sample_out, sizeof(out), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(list.data(), c->splat_list, list.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(state, c->mt_state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyDeviceToHost,
+                           c->stream));
+    if ((rc = end_use(c, c->stream))) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    uint32_t n;
+    std::memcpy(&n, &list[0], 4);
+    if (n > static_cast<uint32_t>(c->splat_cap)) return fail(BDPT_ERR_HIP, "splat list overflow");
+    *nsplats = static_cast<int32_t>(n);
+    if (static_cast<int32_t>(n) > capacity)
+        return fail(BDPT_ERR_INVALID, "splat capacity too small (" + std::to_string(n) + " splats)");
+    for (uint32_t k = 0; k < n; k++) {
+        const float* e = &list[4 + 4 * static_cast<size_t>(k)];
+        std::memcpy(&splats[k].pixel, &e[0], 4);
+        splats[k].rgb[0] = e[1], splats[k].rgb[1] = e[2], splats[k].rgb[2] = e[3];
+    }
     Li[0] = out[0], Li[1] = out[1], Li[2] = out[2];
-    uint32_t used;
-    std::memcpy(&used, &out[3], 4);
-    *draws = static_cast<int32_t>(used);
+    if (taken) std::memcpy(taken, &out[3], 4);
     return BDPT_OK;
+}
+
+int bdpt_sampler_state(uint32_t seed, int64_t draws, uint32_t state[BDPT_MT19937_WORDS]) {
+    if (!state || draws < 0) return fail(BDPT_ERR_INVALID, "bad argument");
+    mt19937_state(seed, draws, state);
+    return BDPT_OK;
+}
+
+int bdpt_render_sample_mt(bdpt_ctx* c, const bdpt_frame_params* p, const float ray[8],
+                          uint32_t state[BDPT_MT19937_WORDS], float Li[3], bdpt_splat* splats, int32_t capacity,
+                          int32_t* nsplats) {
+    return render_bdpt_sample(c, p, ray, state, Li, splats, capacity, nsplats, nullptr);
+}
+
+int bdpt_render_sample(bdpt_ctx* c, const bdpt_frame_params* p, const float ray[8], uint32_t seed,
+                       int32_t* draws, float Li[3], float* fb_host) {
+    if (!c || !p || !draws || !fb_host) return fail(BDPT_ERR_INVALID, "null argument");
+    if (*draws < 0) return fail(BDPT_ERR_INVALID, "negative draw count");
+    uint32_t st[BDPT_MT19937_WORDS], used = 0;
+    mt19937_state(seed, *draws, st);
+    std::vector<bdpt_splat> sp(static_cast<size_t>(std::max(p->rr_depth, 1)));
+    int32_t n = 0;
+    int rc = render_bdpt_sample(c, p, ray, st, Li, sp.data(), static_cast<int32_t>(sp.size()), &n, &used);
+    if (rc) return rc;
+    for (int32_t k = 0; k < n; k++) {  // rgb[pixel] += radiance * misWeight, in the sample's order
+        float* px = fb_host + 3 * static_cast<size_t>(sp[k].pixel);
+        px[0] += sp[k].rgb[0], px[1] += sp[k].rgb[1], px[2] += sp[k].rgb[2];
+    }
+    *draws += static_cast<int32_t>(used);
+    return BDPT_OK;
+}
+
+static int ensure_kat(bdpt_ctx* c, size_t bytes, void** buf) {
+    HIP_TRY(hipMalloc(buf, std::max<size_t>(bytes, 16)));
+    return BDPT_OK;
+}
+
+// Host arrays in, device run, host arrays out (the per-function entry points).
+struct KatBuffers {
+    std::vector<void*> p;
+    ~KatBuffers() {
+        for (void* q : p) (void)hipFree(q);
+    }
+};
+
+static int kat_in(bdpt_ctx* c, KatBuffers& kb, const void* src, size_t bytes, void** dst) {
+    int rc;
+    if ((rc = ensure_kat(c, bytes, dst))) return rc;
+    kb.p.push_back(*dst);
+    if (src && bytes) HIP_TRY(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return BDPT_OK;
+}
+
+static int bsdf_kat(bdpt_ctx* c, int mode, int64_t n, const int32_t* mat, const float* wo, const float* x,
+                    float* out, int out_per) {
+    if (!c || n < 0 || (n > 0 && (!mat || !wo || !x || !out))) return fail(BDPT_ERR_INVALID, "bad argument");
+    for (int64_t i = 0; i < n; i++)
+        if (mat[i] < 0 || mat[i] >= c->sc.nbsdf) return fail(BDPT_ERR_INVALID, "material index out of range");
+    if (n == 0) return BDPT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = begin_use(c, c->stream))) return rc;
+    KatBuffers kb;
+    void *dm, *dwo, *dx, *dout;
+    const size_t N = static_cast<size_t>(n);
+    if ((rc = kat_in(c, kb, mat, 4 * N, &dm)) || (rc = kat_in(c, kb, wo, 12 * N, &dwo)) ||
+        (rc = kat_in(c, kb, x, (mode == 2 ? 8 : 12) * N, &dx)) || (rc = kat_in(c, kb, nullptr, 4 * out_per * N, &dout)))
+        return rc;
+    HIP_TRY(launch_bsdf_kat(c->sc, mode, n, static_cast<const int32_t*>(dm), static_cast<const float*>(dwo),
+                            static_cast<const float*>(dx), static_cast<float*>(dout), c->stream));
+    HIP_TRY(hipMemcpyAsync(out, dout, 4 * out_per * N, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = end_use(c, c->stream))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_bsdf_eval(bdpt_ctx* c, int64_t n, const int32_t* mat, const float* wo, const float* wi, float* f) {
+    return bsdf_kat(c, 0, n, mat, wo, wi, f, 3);
+}
+
+int bdpt_bsdf_pdf(bdpt_ctx* c, int64_t n, const int32_t* mat, const float* wo, const float* wi, float* pdf) {
+    return bsdf_kat(c, 1, n, mat, wo, wi, pdf, 1);
+}
+
+int bdpt_bsdf_sample(bdpt_ctx* c, int64_t n, const int32_t* mat, const float* wo, const float* u, float* f,
+                     float* wi, float* pdf) {
+    if (n > 0 && (!f || !wi || !pdf)) return fail(BDPT_ERR_INVALID, "null output");
+    std::vector<float> o(7 * static_cast<size_t>(std::max<int64_t>(n, 0)));
+    int rc = bsdf_kat(c, 2, n, mat, wo, u, o.data(), 7);
+    if (rc) return rc;
+    for (int64_t i = 0; i < n; i++) {
+        const float* r = &o[7 * static_cast<size_t>(i)];
+        f[3 * i] = r[0], f[3 * i + 1] = r[1], f[3 * i + 2] = r[2];
+        wi[3 * i] = r[3], wi[3 * i + 1] = r[4], wi[3 * i + 2] = r[5];
+        pdf[i] = r[6];
+    }
+    return BDPT_OK;
+}
+
+int bdpt_bsdf_type(const bdpt_scene* s, int32_t mat, uint32_t* type, int32_t* kind) {
+    if (!s || !type || !kind) return fail(BDPT_ERR_INVALID, "null argument");
+    if (mat < 0 || mat >= static_cast<int32_t>(s->layout.bsdfs.size()))
+        return fail(BDPT_ERR_INVALID, "material index out of range");
+    *type = s->layout.bsdfs[static_cast<size_t>(mat)].type;
+    *kind = s->layout.bsdfs[static_cast<size_t>(mat)].kind;
+    return BDPT_OK;
+}
+
+int bdpt_intersect(bdpt_ctx* c, int64_t n, const float* rays, int32_t occlusion, bdpt_hit* out) {
+    static_assert(sizeof(bdpt_hit) == 20 * 4, "bdpt_hit is the kernel's 20-word record");
+    if (!c || n < 0 || (n > 0 && (!rays || !out))) return fail(BDPT_ERR_INVALID, "bad argument");
+    if (n == 0) return BDPT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = begin_use(c, c->stream))) return rc;
+    KatBuffers kb;
+    void *dr, *dout;
+    const size_t N = static_cast<size_t>(n);
+    if ((rc = kat_in(c, kb, rays, 32 * N, &dr)) || (rc = kat_in(c, kb, nullptr, 80 * N, &dout))) return rc;
+    // the traversal-stack overflow columns serve c->nslots rays at a time
+    for (int64_t b = 0; b < n; b += c->nslots) {
+        const int64_t m = std::min<int64_t>(c->nslots, n - b);
+        HIP_TRY(launch_intersect_kat(c->sc, m, occlusion ? 1 : 0, static_cast<const float*>(dr) + 8 * b, c->gstack,
+                                     c->nslots, static_cast<float*>(dout) + 20 * b, c->stream));
+    }
+    HIP_TRY(hipMemcpyAsync(out, dout, 80 * N, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = end_use(c, c->stream))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_splat_to_image_plane(bdpt_ctx* c, const bdpt_frame_params* p, int64_t n, const float* pts, int32_t* xy) {
+    if (!c || !p || n < 0 || (n > 0 && (!pts || !xy))) return fail(BDPT_ERR_INVALID, "bad argument");
+    if (p->width <= 0 || p->height <= 0) return fail(BDPT_ERR_INVALID, "width/height must be > 0");
+    if (n == 0) return BDPT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = begin_use(c, c->stream))) return rc;
+    KatBuffers kb;
+    void *dp, *dxy;
+    const size_t N = static_cast<size_t>(n);
+    if ((rc = kat_in(c, kb, pts, 12 * N, &dp)) || (rc = kat_in(c, kb, nullptr, 8 * N, &dxy))) return rc;
+    HIP_TRY(launch_splat_kat(make_frame(p), n, static_cast<const float*>(dp), static_cast<int32_t*>(dxy), c->stream));
+    HIP_TRY(hipMemcpyAsync(xy, dxy, 8 * N, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = end_use(c, c->stream))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+// Device-only diagnostics without a scene (synchronous, default stream).
+static int device_kat(int32_t device, size_t in_bytes, const float* in, size_t in2_bytes, const float* in2,
+                      size_t out_bytes, float* out,
+                      hipError_t (*launch)(const float*, const float*, float*)) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(BDPT_ERR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= count) return fail(BDPT_ERR_INVALID, "bad device");
+    HIP_TRY(hipSetDevice(device));
+    float *a = nullptr, *b = nullptr, *o = nullptr;
+    hipError_t e = hipMalloc(&a, std::max<size_t>(in_bytes, 16));
+    if (e == hipSuccess) e = hipMalloc(&b, std::max<size_t>(in2_bytes, 16));
+    if (e == hipSuccess) e = hipMalloc(&o, std::max<size_t>(out_bytes, 16));
+    if (e == hipSuccess) e = hipMemcpy(a, in, in_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && in2) e = hipMemcpy(b, in2, in2_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch(a, b, o);
+    if (e == hipSuccess) e = hipMemcpy(out, o, out_bytes, hipMemcpyDeviceToHost);
+    for (float* q : {a, b, o})
+        if (q) (void)hipFree(q);
+    if (e != hipSuccess) return fail(BDPT_ERR_HIP, std::string("device diagnostic: ") + hipGetErrorString(e));
+    return BDPT_OK;
+}
+
+static thread_local int64_t g_kat_n = 0;
+
+int bdpt_debug_fresnel(int32_t device, int64_t n, const float* in, float* out) {
+    if (n < 0 || (n > 0 && (!in || !out))) return fail(BDPT_ERR_INVALID, "bad argument");
+    if (n == 0) return BDPT_OK;
+    g_kat_n = n;
+    const size_t N = static_cast<size_t>(n);
+    return device_kat(device, 16 * N, in, 0, nullptr, 4 * N, out, [](const float* a, const float*, float* o) {
+        return launch_fresnel_kat(g_kat_n, a, o, nullptr);
+    });
+}
+
+int bdpt_debug_triangle(int32_t device, int64_t n, const float* rays, const float* verts, float* out) {
+    if (n < 0 || (n > 0 && (!rays || !verts || !out))) return fail(BDPT_ERR_INVALID, "bad argument");
+    if (n == 0) return BDPT_OK;
+    g_kat_n = n;
+    const size_t N = static_cast<size_t>(n);
+    return device_kat(device, 32 * N, rays, 36 * N, verts, 16 * N, out, [](const float* a, const float* b, float* o) {
+        return launch_triangle_kat(g_kat_n, a, b, o, nullptr);
+    });
 }
 
 }  // extern "C"

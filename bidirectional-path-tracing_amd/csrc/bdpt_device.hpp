@@ -240,6 +240,31 @@ __device__ __forceinline__ uint32_t mt_ring_step(LazyMT& m, uint32_t seed, uint3
     return mt_temper(v);
 }
 
+#ifndef BDPT_SAMPLER_STATE
+#define BDPT_SAMPLER_STATE 0  // 1: the single-sample build (sample_state.hip): draws from a caller's std::mt19937
+#endif
+#if BDPT_SAMPLER_STATE
+// The single-sample entry points (Integrator::render(const Ray&, Sampler&),
+// integrator.h:31) take the caller's whole std::mt19937 (Sampler::g, math.h:63-76):
+// libstdc++'s _M_x[624] then _M_p, in the order its operator<< writes them. It is
+// advanced exactly as mersenne_twister_engine::operator() does (random.tcc:
+// _M_gen_rand when _M_p reaches 624, then tempering). One lane uses it; the
+// state lives in global memory, its address in LDS header words 0-1.
+__device__ BDPT_NOINLINE uint32_t mt_state_u32() {
+    const uint64_t base = (static_cast<uint64_t>(g_scene_lds[1]) << 32) | g_scene_lds[0];
+    uint32_t* const x = reinterpret_cast<uint32_t*>(base);
+    uint32_t p = x[624];
+    if (p >= 624u) {
+        for (int k = 0; k < 227; k++) x[k] = mt_twist(x[k], x[k + 1], x[k + 397]);
+        for (int k = 227; k < 623; k++) x[k] = mt_twist(x[k], x[k + 1], x[k - 227]);
+        x[623] = mt_twist(x[623], x[0], x[396]);
+        p = 0;
+    }
+    x[624] = p + 1;
+    return mt_temper(x[p]);
+}
+#endif
+
 // x[0] (the seed) from x[i]: the seeding step x -> 1812433253 (x ^ x >> 30) + i
 // is a bijection (odd multiplier; a 30-bit xorshift undoes itself).
 __device__ __forceinline__ uint32_t mt_seed_from(uint32_t x, uint32_t i) {
@@ -272,7 +297,10 @@ __device__ BDPT_NOINLINE uint32_t mt_u32_long(LazyMT& r) {
 
 // generate_canonical<float, 24> (libstdc++ 11 random.tcc:3348-3380).
 __device__ __forceinline__ float next1(LazyMT& r) {
-#if BDPT_DEEP_RNG
+#if BDPT_SAMPLER_STATE
+    const uint32_t u = mt_state_u32();
+    r.n++;
+#elif BDPT_DEEP_RNG
     const uint32_t u = r.n < 227 ? mt_next_u32(r) : mt_u32_long(r);
 #else
     const uint32_t u = mt_next_u32(r);
@@ -457,7 +485,7 @@ __device__ __forceinline__ bool box_test(float lx, float ly, float lz, float hx,
 // rayTriangleIntersect (core.h:379-400) + accel.h:43's t > 1e-3, on the
 // triangle's v0 and edges (e1 = v1 - v0, e2 = v2 - v0 rounded as the
 // reference rounds them).
-__device__ __forceinline__ bool tri_test_edges(f3 v0, f3 e1, f3 e2, const Ray& r, float& t, float& u, float& v) {
+__device__ __forceinline__ bool tri_test_raw(f3 v0, f3 e1, f3 e2, const Ray& r, float& t, float& u, float& v) {
     const f3 pvec = cross(r.d, e2);
     const float det = dot(e1, pvec);
     if (fabsf(det) < kEpsilon) return false;
@@ -469,7 +497,10 @@ __device__ __forceinline__ bool tri_test_edges(f3 v0, f3 e1, f3 e2, const Ray& r
     v = dot(r.d, qvec) * invDet;
     if (v < 0.f || u + v > 1.f) return false;
     t = dot(e2, qvec) * invDet;
-    return t >= kTriMinT;
+    return true;
+}
+__device__ __forceinline__ bool tri_test_edges(f3 v0, f3 e1, f3 e2, const Ray& r, float& t, float& u, float& v) {
+    return tri_test_raw(v0, e1, e2, r, t, u, v) && t >= kTriMinT;
 }
 __device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_t i, const Ray& r, float& t, float& u,
                                          float& v) {

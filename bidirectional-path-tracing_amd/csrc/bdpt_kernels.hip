@@ -61,6 +61,7 @@ __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame
     }
 }
 
+#if !BDPT_SAMPLER_STATE
 // Kernel parameters live in a small device buffer; the loop re-derives its
 // pointer to them every iteration (through an empty asm) so the compiler loads
 // the rarely used camera / frame constants at their point of use instead of
@@ -239,11 +240,16 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     }
 }
 
-// One Integrator::render(ray, sampler) call on one lane. out = Li.xyz, draws.
+#endif  // !BDPT_SAMPLER_STATE
+
+#if BDPT_SAMPLER_STATE
+// One Integrator::render(ray, sampler) call on one lane (single-sample build,
+// sample_state.hip): the sampler is the caller's std::mt19937 state, whose
+// address sc.mt_ring carries into the LDS header (mt_state_u32); splats go to
+// the list `fb` (splat_add). out = Li.xyz, draws taken.
 __global__ __launch_bounds__(64) void bdpt_sample_kernel(DevScene sc, DevFrame fr, float* __restrict__ fb,
                                                          float* __restrict__ lvbuf, uint2* __restrict__ gstack,
-                                                         Ray ray, uint32_t seed, uint32_t draws,
-                                                         float* __restrict__ out) {
+                                                         Ray ray, float* __restrict__ out) {
     __shared__ uint2 stack_mem[kLdsStack * 64];
     scene_tables_to_lds(sc);
     if (threadIdx.x != 0) return;
@@ -251,7 +257,7 @@ __global__ __launch_bounds__(64) void bdpt_sample_kernel(DevScene sc, DevFrame f
     const LightStore ls = light_store(lvbuf, fr.rr_depth, 0);
     __shared__ LaneCold cold_mem[1];
     Lane L(cold_mem[0]);
-    mt_seed_skip(L.rng, seed, draws);
+    L.rng = LazyMT{0u, 0u, 0u, 0u};  // unused: next1 draws from the caller's state
     L.c.pixel = 0;
     L.c.cam_d = ray.d;
     L.ray = ray;
@@ -266,9 +272,12 @@ __global__ __launch_bounds__(64) void bdpt_sample_kernel(DevScene sc, DevFrame f
     out[3] = __uint_as_float(L.rng.n);
 }
 
+#endif  // BDPT_SAMPLER_STATE
+
 }  // namespace dev
 
 // ------------------------------------------------------------ host launchers
+#if !BDPT_SAMPLER_STATE
 size_t frame_params_bytes() { return sizeof(dev::KParams); }
 
 // `dparams` is a device buffer of frame_params_bytes() owned by the caller; it
@@ -290,13 +299,18 @@ hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float*
     return hipGetLastError();
 }
 
-hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
-                         const dev::Ray& ray, uint32_t seed, uint32_t draws, float* out, hipStream_t stream) {
+#endif  // !BDPT_SAMPLER_STATE
+
+#if BDPT_SAMPLER_STATE
+// sc.mt_ring = the device copy of the caller's std::mt19937 state (625 words);
+// splats = the splat list (header + records, see splat_add).
+hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* splats, float* lvbuf, uint2* gstack,
+                         const dev::Ray& ray, float* out, hipStream_t stream) {
     hipLaunchKernelGGL(dev::bdpt_sample_kernel, dim3(1), dim3(64), 4 * static_cast<size_t>(sc.lds_words), stream, sc,
-                       fr, fb, lvbuf, gstack, ray, seed,
-                       draws, out);
+                       fr, splats, lvbuf, gstack, ray, out);
     return hipGetLastError();
 }
+#else
 
 // Resident 256-lane blocks per CU for the frame kernel (VGPR and LDS limited).
 int frame_kernel_blocks_per_cu(size_t dyn_lds) {
@@ -311,5 +325,7 @@ int frame_kernel_blocks_per_cu(size_t dyn_lds) {
 int frame_kernel_lds_stack() { return dev::kLdsStack; }
 int frame_kernel_block() { return dev::kBlock; }
 int light_vertex_fields() { return dev::kLvFields; }
+
+#endif  // BDPT_SAMPLER_STATE
 
 }  // namespace bdpt

@@ -215,6 +215,27 @@ struct Lane {
     __device__ explicit Lane(LaneCold& cold) : c(cold) {}
 };
 
+// rgb[pixel] += radiance * misWeight under the pixel's lock (bdpt.h:363-370).
+// The single-sample build returns the splats of its one sample as a list
+// instead (fb = header {count, capacity, 0, 0} then (pixel, r, g, b) records),
+// so the caller adds them to its own framebuffer in the reference's order.
+__device__ __forceinline__ void splat_add(float* __restrict__ fb, int pixel, f3 v) {
+#if BDPT_SAMPLER_STATE
+    uint32_t* const hdr = reinterpret_cast<uint32_t*>(fb);
+    const uint32_t k = hdr[0];
+    hdr[0] = k + 1;
+    if (k < hdr[1]) {
+        float* e = fb + 4 + 4 * static_cast<size_t>(k);
+        e[0] = __int_as_float(pixel), e[1] = v.x, e[2] = v.y, e[3] = v.z;
+    }
+#else
+    float* px = fb + 3 * static_cast<size_t>(pixel);
+    atomicAdd(px + 0, v.x);
+    atomicAdd(px + 1, v.y);
+    atomicAdd(px + 2, v.z);
+#endif
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __restrict__ fb, Counts& cnt) {
     if (COUNT) cnt.c[7] += L.rng.n;
@@ -571,10 +592,7 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
         case ST_SPLAT:
             if (!hit) {
                 if (COUNT) cnt.c[6]++;
-                float* px = fb + 3 * static_cast<size_t>(L.c.pend_px);
-                atomicAdd(px + 0, L.c.pend.x);
-                atomicAdd(px + 1, L.c.pend.y);
-                atomicAdd(px + 2, L.c.pend.z);
+                splat_add(fb, L.c.pend_px, L.c.pend);
             }
             act = A_LIGHT_CONTINUE;
             break;

@@ -35,7 +35,12 @@ struct PtRng {
 // Output n >= 227 of std::mt19937(seed) from the lane's ring (mt_ring_step).
 __device__ BDPT_NOINLINE uint32_t pt_u32_slow(PtRng& r) { return mt_ring_step(r.m, r.seed, r.ring, r.stride); }
 __device__ __forceinline__ float next1(PtRng& r) {
+#if BDPT_SAMPLER_STATE
+    const uint32_t u = mt_state_u32();  // the caller's std::mt19937 (single-sample build)
+    r.m.n++;
+#else
     const uint32_t u = r.m.n < 227 ? mt_next_u32(r.m) : pt_u32_slow(r);
+#endif
     const float f = static_cast<float>(u) / 4294967296.0f;  // generate_canonical (random.tcc:3348-3380)
     return f >= 1.0f ? 0x1.fffffep-1f : f;
 }
@@ -601,6 +606,7 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
     }
 }
 
+#if !BDPT_SAMPLER_STATE
 template <bool COUNT, bool OVERLAP>
 __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const PtParams* __restrict__ pp) {
     const PtParams& P = *pp;
@@ -700,11 +706,15 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
     if (COUNT) flush_counts(cnt, P.counters);
 }
 
+#endif  // !BDPT_SAMPLER_STATE
+
+#if BDPT_SAMPLER_STATE
 // One PathTracerIntegrator / DirectIntegrator::render(ray, sampler) call on one
-// lane (path.h:235-245, direct.h:449-462): the sampler is std::mt19937(seed)
-// after `draws` outputs (< 227). out = Li.xyz, draws after the call.
-__global__ __launch_bounds__(64) void pt_sample_kernel(const PtParams* __restrict__ pp, Ray ray, uint32_t seed,
-                                                       uint32_t draws, float* __restrict__ out) {
+// lane (path.h:235-245, direct.h:449-462), single-sample build (sample_state.hip):
+// the sampler is the caller's std::mt19937 state (P.sc.mt_ring, mt_state_u32).
+// out = Li.xyz, draws taken.
+__global__ __launch_bounds__(64) void pt_sample_kernel(const PtParams* __restrict__ pp, Ray ray,
+                                                       float* __restrict__ out) {
     const PtParams& P = *pp;
     __shared__ uint2 stack_mem[kLdsStack * 64];
     scene_tables_to_lds(P.sc);
@@ -715,8 +725,8 @@ __global__ __launch_bounds__(64) void pt_sample_kernel(const PtParams* __restric
     PtLane L;
     L.rng.ring = P.ring;
     L.rng.stride = 1;
-    L.rng.seed = seed;
-    mt_seed_skip(L.rng.m, seed, draws);
+    L.rng.seed = 0;
+    L.rng.m = LazyMT{0u, 0u, 0u, 0u};  // unused: next1 draws from the caller's state
     L.pixel = 0;
     L.ray = ray;
     L.q = PQ_PRIMARY;
@@ -729,9 +739,12 @@ __global__ __launch_bounds__(64) void pt_sample_kernel(const PtParams* __restric
     out[3] = __uint_as_float(L.rng.m.n);
 }
 
+#endif  // BDPT_SAMPLER_STATE
+
 }  // namespace dev
 
 // ------------------------------------------------------------ host side
+#if !BDPT_SAMPLER_STATE
 size_t pt_params_bytes() { return sizeof(dev::PtParams); }
 int pt_block() { return 256; }
 int pt_lds_stack() { return dev::kLdsStack; }
@@ -772,10 +785,11 @@ hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int
     return hipGetLastError();
 }
 
+#else
+// sc.mt_ring = the device copy of the caller's std::mt19937 state (625 words).
 hipError_t launch_pt_sample(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8],
-                            float4* levels, uint32_t* ring, uint2* gstack, const dev::Ray& ray, uint32_t seed,
-                            uint32_t draws, float* out, unsigned long long* counters, hipStream_t stream,
-                            void* dparams) {
+                            float4* levels, uint32_t* ring, uint2* gstack, const dev::Ray& ray, float* out,
+                            unsigned long long* counters, hipStream_t stream, void* dparams) {
     dev::PtParams host{};
     host.sc = sc;
     host.fr = fr;
@@ -793,8 +807,9 @@ hipError_t launch_pt_sample(const dev::DevScene& sc, const dev::DevFrame& fr, co
     if (e != hipSuccess) return e;
     const dev::PtParams* kp = static_cast<const dev::PtParams*>(dparams);
     hipLaunchKernelGGL(dev::pt_sample_kernel, dim3(1), dim3(64), 4 * static_cast<size_t>(sc.lds_words), stream, kp,
-                       ray, seed, draws, out);
+                       ray, out);
     return hipGetLastError();
 }
+#endif  // BDPT_SAMPLER_STATE
 
 }  // namespace bdpt

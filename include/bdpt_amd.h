@@ -15,8 +15,16 @@
  *                            calling BDPTIntegrator::render bdpt.h:219-241 for every
  *                            (pixel, sample), with camera splats (bdpt.h:295-371)
  *                            accumulated into the same framebuffer
- *   bdpt_render_sample       virtual v3f Integrator::render(const Ray&, Sampler&) const
- *                            src/core/integrator.h:48, overridden at bdpt.h:219
+ *   bdpt_render_sample_mt    virtual v3f Integrator::render(const Ray&, Sampler&) const
+ *                            src/core/integrator.h:31, overridden at bdpt.h:219, with the
+ *                            caller's Sampler (std::mt19937 state, src/core/math.h:63-76)
+ *   bdpt_render_sample       the same, Sampler given as (seed, draws already taken)
+ *   bdpt_bsdf_eval/pdf/sample  BSDF::eval / pdf / sample        src/core/core.h:308-310
+ *                            (diffuse.h:35-61, perfectmirror.h:33-59, glass.h:55-108,
+ *                             mixture.h:60-151, phong.h) of a scene material, batched
+ *   bdpt_intersect           AcceleratorBVH::intersect / occlusion  src/core/accel.h:125-172,
+ *                            externals/bvh.h:259-352 (as visibilityQuery calls it, bdpt.h:498-505)
+ *   bdpt_splat_to_image_plane  BDPTIntegrator::splatToImagePlane   bdpt.h:485-496
  *   bdpt_ctx_destroy         Integrator/Renderer teardown (renderer.cpp:221-227)
  *   bdpt_config_load_toml    loadTOML                         src/main.cpp:22-116
  *   bdpt_save_exr            Integrator::save -> saveEXR      integrator.cpp:26-30, utils.h:95-156
@@ -29,8 +37,12 @@
  *
  * Conventions: plain C types only; status 0 = OK, < 0 = error (message from
  * bdpt_last_error(), thread-local). A context is bound to one HIP device and is
- * not thread-safe. Nothing here falls back to the CPU: without a HIP device,
- * bdpt_ctx_create fails with BDPT_ERR_NO_DEVICE.
+ * not thread-safe: callers that render from several threads (the reference's
+ * parallel_for, renderer.cpp:157) keep one context per thread. Calls on one
+ * context are ordered even across streams (each call waits for the previous
+ * call's work on its stream before touching the context's buffers). Nothing
+ * here falls back to the CPU: without a HIP device, bdpt_ctx_create fails with
+ * BDPT_ERR_NO_DEVICE.
  *
  * Determinism: camera sample (pixel p, sample k) draws from
  * std::mt19937(seed_base + p*spp + k) exactly like the reference's Sampler
@@ -143,9 +155,30 @@ int bdpt_ctx_destroy(bdpt_ctx* ctx);
 int bdpt_render(bdpt_ctx* ctx, const bdpt_frame_params* params, float* fb_device, void* hip_stream);
 /* Same, with a host framebuffer (copied to the device, accumulated, copied back). Synchronous. */
 int bdpt_render_host(bdpt_ctx* ctx, const bdpt_frame_params* params, float* fb_host);
-/* One camera sample through BDPTIntegrator::render(ray, sampler): ray = o.xyz d.xyz
- * min_t max_t; the sampler is std::mt19937(sampler_seed) after *sampler_draws
- * draws (updated on return). Returns Li; splats are added to fb_host. Synchronous. */
+/* ---- Integrator::render(const Ray&, Sampler&): one camera sample ---- */
+/* The reference's Sampler (math.h:63-76) is a std::mt19937 plus a stateless
+ * uniform_real_distribution<float>. Its state crosses the ABI as libstdc++ streams
+ * it (operator<< / operator>> of std::mersenne_twister_engine): the 624 state words
+ * _M_x, then the position _M_p (0..624). */
+#define BDPT_MT19937_WORDS 625
+typedef struct {
+    int32_t pixel; /* index into the W*H framebuffer (row-major, row 0 = top) */
+    float rgb[3];  /* radiance * misWeight, added as rgb[pixel] += ... (bdpt.h:363-370) */
+} bdpt_splat;
+/* The state of std::mt19937(seed) after `draws` outputs (host only). */
+int bdpt_sampler_state(uint32_t seed, int64_t draws, uint32_t state[BDPT_MT19937_WORDS]);
+/* BDPTIntegrator::render(ray, sampler) (bdpt.h:219-241): ray = o.xyz d.xyz min_t max_t;
+ * `state` is the caller's sampler, advanced in place exactly as the reference
+ * advances it. Returns Li; the camera splats of the sample's light subpath are
+ * returned in order in splats[0 .. *nsplats) (at most rr_depth; BDPT_ERR_INVALID
+ * if `capacity` is smaller than the count) for the caller to add to its image.
+ * Any rr_depth in [1, 1024]. Synchronous. */
+int bdpt_render_sample_mt(bdpt_ctx* ctx, const bdpt_frame_params* params, const float ray[8],
+                          uint32_t state[BDPT_MT19937_WORDS], float Li[3], bdpt_splat* splats, int32_t capacity,
+                          int32_t* nsplats);
+/* The same with the sampler given as std::mt19937(sampler_seed) after
+ * *sampler_draws draws (updated on return); splats are added to fb_host
+ * (W*H*3 floats) in order. Synchronous. */
 int bdpt_render_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, const float ray[8], uint32_t sampler_seed,
                        int32_t* sampler_draws, float Li[3], float* fb_host);
 int bdpt_get_stats(bdpt_ctx* ctx, bdpt_stats* out);
@@ -173,9 +206,12 @@ int bdpt_render_path(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_
                      void* hip_stream);
 int bdpt_render_path_host(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_path_params* path,
                           float* fb_host);
-/* One PathTracerIntegrator::render(ray, sampler) call (path.h:235-245): ray = o.xyz
- * d.xyz min_t max_t; the sampler is std::mt19937(sampler_seed) after *sampler_draws
- * (< 227) draws, updated on return. Returns Li. Synchronous. */
+/* One PathTracerIntegrator::render(ray, sampler) call (path.h:235-245) with the
+ * caller's sampler state (advanced in place, as bdpt_render_sample_mt). Synchronous. */
+int bdpt_render_path_sample_mt(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_path_params* path,
+                               const float ray[8], uint32_t state[BDPT_MT19937_WORDS], float Li[3]);
+/* The same with the sampler given as std::mt19937(sampler_seed) after
+ * *sampler_draws draws, updated on return. */
 int bdpt_render_path_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_path_params* path,
                             const float ray[8], uint32_t sampler_seed, int32_t* sampler_draws, float Li[3]);
 
@@ -201,13 +237,53 @@ int bdpt_render_direct(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdp
 int bdpt_render_direct_host(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_direct_params* direct,
                             float* fb_host);
 /* One DirectIntegrator::render(ray, sampler) call (direct.h:449-462), as
- * bdpt_render_path_sample. */
+ * bdpt_render_path_sample_mt / bdpt_render_path_sample. */
+int bdpt_render_direct_sample_mt(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_direct_params* direct,
+                                 const float ray[8], uint32_t state[BDPT_MT19937_WORDS], float Li[3]);
 int bdpt_render_direct_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, const bdpt_direct_params* direct,
                               const float ray[8], uint32_t sampler_seed, int32_t* sampler_draws, float Li[3]);
 /* samplingStrategy string -> BDPT_DIRECT_* (0 when unknown). */
 int32_t bdpt_direct_strategy(const char* name);
 
+/* ---- the BSDF plugin contract and the path's building blocks, batched on the device ---- */
+/* All arrays are host arrays of n elements; directions are in the local shading
+ * frame (z = the shading normal) as SurfaceInteraction::wo / wi. Synchronous. */
+/* BSDF::eval(i) of material mat[k]: f * cos(wi) (core.h:308). f: n x 3. */
+int bdpt_bsdf_eval(bdpt_ctx* ctx, int64_t n, const int32_t* mat, const float* wo, const float* wi, float* f);
+/* BSDF::pdf(i): the solid-angle pdf of wi (core.h:309). */
+int bdpt_bsdf_pdf(bdpt_ctx* ctx, int64_t n, const int32_t* mat, const float* wo, const float* wi, float* pdf);
+/* BSDF::sample(i, u, &pdf) (core.h:310): u = n x 2 samples in [0, 1); returns f * cos
+ * (f: n x 3), the sampled wi (n x 3) and *pdf. */
+int bdpt_bsdf_sample(bdpt_ctx* ctx, int64_t n, const int32_t* mat, const float* wo, const float* u, float* f,
+                     float* wi, float* pdf);
+/* BSDF::getType() (core.h:311) of a scene material, and this build's kind
+ * (1 diffuse, 2 mirror, 3 glass, 4 mixture, 5 phong, 0 the null BSDF of illum 5). */
+int bdpt_bsdf_type(const bdpt_scene* scene, int32_t mat, uint32_t* type, int32_t* kind);
+
+/* A closest hit as AcceleratorBVH::intersect fills SurfaceInteraction (accel.h:125-172). */
+typedef struct {
+    int32_t hit;               /* closest hit accepted (min_t <= t <= max_t) / occluded */
+    float t, u, v;             /* t is the search result even when not accepted (accel.h:132) */
+    int32_t shape_id, prim_id, mat_id;
+    float p[3], ns[3], ng[3];  /* hit point, frameNs.n, frameNg.n */
+    float wo[3];               /* frameNs.toLocal(-ray.d) */
+    int32_t tri;               /* this build's triangle index (reference BVH leaf order) */
+} bdpt_hit;
+/* rays: n x 8 (o.xyz d.xyz min_t max_t). occlusion = 0: closest hit (accel.h:125);
+ * 1: the any-hit query of visibilityQuery (bvh.h:259-352 with occlusion = true),
+ * result in hit only. */
+int bdpt_intersect(bdpt_ctx* ctx, int64_t n, const float* rays, int32_t occlusion, bdpt_hit* out);
+/* BDPTIntegrator::splatToImagePlane (bdpt.h:485-496) of points p (n x 3) for the
+ * camera and image of params: xy = n x 2 (the reference's int truncation). */
+int bdpt_splat_to_image_plane(bdpt_ctx* ctx, const bdpt_frame_params* params, int64_t n, const float* p,
+                              int32_t* xy);
+
 /* ---- diagnostics ---- */
+/* GlassBSDF::FresnelDielectric (glass.h:40-53): in = n x (eta_i, eta_t, cos_i, cos_t). */
+int bdpt_debug_fresnel(int32_t device, int64_t n, const float* in, float* out);
+/* rayTriangleIntersect (core.h:379-400): rays n x 8, verts n x 9 (v0 v1 v2);
+ * out = n x (hit, t, u, v). */
+int bdpt_debug_triangle(int32_t device, int64_t n, const float* rays, const float* verts, float* out);
 /* The device restatements of glibc's transcendental functions the path uses
  * (std::sinf / cosf / powf in src/core/math.h:125-242, mixture.h:70), element-wise
  * on device `device`: fn 0 sinf(x), 1 cosf(x), 2 powf(x, y), 3 / 4 the sin / cos

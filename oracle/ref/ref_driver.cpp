@@ -21,6 +21,9 @@
 //   ref_bdpt dump   <scene.toml> W H OUTDIR       (scene / BVH / camera dump)
 //   ref_bdpt exr    <fb.f32> W H <out.exr>        (the reference's saveEXR, utils.h:95-156)
 //   ref_bdpt toml   <scene.toml>                  (the reference's loadTOML, main.cpp:22-116, as JSON)
+//   ref_bdpt kat    <scene.toml> W H KIND in.f32 out.f32   (per-function known answers, cmdKat)
+//   ref_bdpt sample_state <scene.toml> W H SPP RR in.f32 out.f32 -   (render(ray, sampler) from a
+//                                                  given std::mt19937 state, cmdSampleState)
 
 #define main tinyrender_reference_main
 #include "main.cpp"   // reference src/main.cpp: loadTOML, g_FrameBufferLocks, tinyobj/tinyexr impl
@@ -356,6 +359,187 @@ int cmdToml(int argc, char** argv) {
     return 0;
 }
 
+std::vector<float> readF32(const std::string& path) {
+    std::vector<float> v;
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return v;
+    fseek(f, 0, SEEK_END);
+    const long n = ftell(f) / 4;
+    fseek(f, 0, SEEK_SET);
+    v.resize((size_t)n);
+    if (fread(v.data(), 4, (size_t)n, f) != (size_t)n) v.clear();
+    fclose(f);
+    return v;
+}
+
+inline int f2i(float x) {
+    int i;
+    memcpy(&i, &x, 4);
+    return i;
+}
+inline float i2f(int i) {
+    float x;
+    memcpy(&x, &i, 4);
+    return x;
+}
+
+// Per-function known-answer outputs of the reference's own functions on
+// records read from a float32 file (test fixtures, tests/golden/make_kat_goldens.py):
+//   bsdf      in (mat, wo[3], wi[3], u[2])  out (eval[3], pdf, sample f[3], wi[3], pdf, type, null)
+//             BSDF::eval / pdf / sample (core.h:308-310) of scene material mat
+//   fresnel   in (eta_i, eta_t, cos_i, cos_t)   out F    GlassBSDF::FresnelDielectric (glass.h:40-53)
+//   tri       in (ray[8], v0 v1 v2)  out (hit, t, u, v)  rayTriangleIntersect (core.h:379-400)
+//   intersect in ray[8]  out (hit, t, u, v, shapeID, primID, matID, p[3], frameNs.n[3], frameNg.n[3],
+//             wo[3], -1, occluded)   AcceleratorBVH::intersect (accel.h:125-172) and the any-hit
+//             query visibilityQuery makes (bvh.h:259-352, occlusion = true)
+//   splat     in p[3]  out (x, y) as int bits   BDPTIntegrator::splatToImagePlane (bdpt.h:485-496)
+int cmdKat(int argc, char** argv) {
+    if (argc < 8) return 2;
+    const std::string toml = argv[2], kind = argv[5];
+    const int W = atoi(argv[3]), H = atoi(argv[4]);
+    Setup s;
+    setup(s, toml, W, H, 1, 0);
+    const std::vector<float> in = readF32(argv[6]);
+    std::vector<float> out;
+    const Scene& sc = *s.scene;
+    if (kind == "bsdf") {
+        for (size_t r = 0; r + 9 <= in.size(); r += 9) {
+            const int mat = f2i(in[r]);
+            const BSDF* b = sc.bsdfs[mat].get();
+            float o[14] = {0};
+            if (!b) {
+                o[13] = 1.f;  // illum 5: the reference keeps a null BSDF
+            } else {
+                SurfaceInteraction si;
+                si.wo = v3f(in[r + 1], in[r + 2], in[r + 3]);
+                si.wi = v3f(in[r + 4], in[r + 5], in[r + 6]);
+                si.matID = mat;
+                const v3f f = b->eval(si);
+                const float pdf = b->pdf(si);
+                SurfaceInteraction so = si;
+                float spdf = 0.f;
+                const v3f sf = b->sample(so, v2f(in[r + 7], in[r + 8]), &spdf);
+                const float vals[13] = {f.x, f.y, f.z, pdf, sf.x, sf.y, sf.z, so.wi.x, so.wi.y, so.wi.z, spdf,
+                                        i2f((int)b->getType()), 0.f};
+                memcpy(o, vals, sizeof(vals));
+            }
+            out.insert(out.end(), o, o + 14);
+        }
+    } else if (kind == "fresnel") {
+        const GlassBSDF* g = nullptr;
+        for (const auto& b : sc.bsdfs)
+            if (!g && b) g = dynamic_cast<const GlassBSDF*>(b.get());
+        if (!g) { fprintf(stderr, "no glass material\n"); return 2; }
+        for (size_t r = 0; r + 4 <= in.size(); r += 4) out.push_back(g->FresnelDielectric(in[r], in[r + 1], in[r + 2], in[r + 3]));
+    } else if (kind == "tri") {
+        for (size_t r = 0; r + 17 <= in.size(); r += 17) {
+            const Ray ray(v3f(in[r], in[r + 1], in[r + 2]), v3f(in[r + 3], in[r + 4], in[r + 5]), in[r + 6], in[r + 7]);
+            float t = 0.f, u = 0.f, v = 0.f;
+            const bool hit = rayTriangleIntersect(ray, v3f(in[r + 8], in[r + 9], in[r + 10]),
+                                                  v3f(in[r + 11], in[r + 12], in[r + 13]),
+                                                  v3f(in[r + 14], in[r + 15], in[r + 16]), t, u, v);
+            const float o[4] = {hit ? 1.f : 0.f, t, u, v};
+            out.insert(out.end(), o, o + 4);
+        }
+    } else if (kind == "intersect") {
+        for (size_t r = 0; r + 8 <= in.size(); r += 8) {
+            const Ray ray(v3f(in[r], in[r + 1], in[r + 2]), v3f(in[r + 3], in[r + 4], in[r + 5]), in[r + 6], in[r + 7]);
+            SurfaceInteraction si;
+            const bool hit = sc.bvh->intersect(ray, si);
+            IntersectionInfo ii = IntersectionInfo();
+            const bool occ = sc.bvh->bvh->getIntersection(ray, &ii, true);
+            float o[21] = {0};
+            o[0] = hit ? 1.f : 0.f;
+            o[1] = si.t;
+            if (hit) {
+                o[2] = si.u, o[3] = si.v;
+                o[4] = i2f((int)si.shapeID), o[5] = i2f((int)si.primID), o[6] = i2f(si.matID);
+                o[7] = si.p.x, o[8] = si.p.y, o[9] = si.p.z;
+                o[10] = si.frameNs.n.x, o[11] = si.frameNs.n.y, o[12] = si.frameNs.n.z;
+                o[13] = si.frameNg.n.x, o[14] = si.frameNg.n.y, o[15] = si.frameNg.n.z;
+                o[16] = si.wo.x, o[17] = si.wo.y, o[18] = si.wo.z;
+            }
+            o[19] = i2f(-1);
+            o[20] = occ ? 1.f : 0.f;
+            out.insert(out.end(), o, o + 21);
+        }
+    } else if (kind == "splat") {
+        const BDPTIntegrator* bi = dynamic_cast<const BDPTIntegrator*>(s.integ.get());
+        if (!bi) { fprintf(stderr, "splat needs a bdpt scene\n"); return 2; }
+        for (size_t r = 0; r + 3 <= in.size(); r += 3) {
+            int x = 0, y = 0;
+            bi->splatToImagePlane(v3f(in[r], in[r + 1], in[r + 2]), x, y);
+            out.push_back(i2f(x));
+            out.push_back(i2f(y));
+        }
+    } else {
+        fprintf(stderr, "unknown kat kind\n");
+        return 2;
+    }
+    writeBin(argv[7], out.data(), out.size() * 4);
+    printf("{\"records\": %zu}\n", out.size());
+    return 0;
+}
+
+// Integrator::render(const Ray&, Sampler&) (integrator.h:31) with an arbitrary
+// sampler state: records of (ray[8], std::mt19937 state as 625 words = what
+// libstdc++'s operator<< writes: _M_x[624], _M_p). Out per record: Li[3],
+// the state after the call (625 words), then the image's non-zero pixels
+// after the call (camera splats; rgb cleared first): count, then up to 16
+// (pixel, r, g, b) in pixel order.
+int cmdSampleState(int argc, char** argv) {
+    if (argc < 10) return 2;
+    const std::string toml = argv[2];
+    const int W = atoi(argv[3]), H = atoi(argv[4]), spp = atoi(argv[5]), rr = atoi(argv[6]);
+    Setup s;
+    setup(s, toml, W, H, spp, rr);
+    const std::vector<float> in = readF32(argv[7]);
+    const size_t rec = 8 + 625;
+    std::vector<float> out;
+    for (size_t r = 0; r + rec <= in.size(); r += rec) {
+        const Ray ray(v3f(in[r], in[r + 1], in[r + 2]), v3f(in[r + 3], in[r + 4], in[r + 5]), in[r + 6], in[r + 7]);
+        std::ostringstream os;
+        for (int k = 0; k < 625; k++) {
+            uint32_t w;
+            memcpy(&w, &in[r + 8 + k], 4);
+            os << w << ' ';
+        }
+        Sampler sampler(0);
+        std::istringstream is(os.str());
+        is >> sampler.g;
+        s.integ->rgb->clear();
+        const v3f Li = s.integ->render(ray, sampler);
+        out.push_back(Li.x), out.push_back(Li.y), out.push_back(Li.z);
+        std::ostringstream so;
+        so << sampler.g;
+        std::istringstream si(so.str());
+        for (int k = 0; k < 625; k++) {
+            unsigned long long w = 0;
+            si >> w;
+            uint32_t w32 = (uint32_t)w;
+            float f;
+            memcpy(&f, &w32, 4);
+            out.push_back(f);
+        }
+        std::vector<float> sp;
+        int n = 0;
+        for (int p = 0; p < W * H; p++) {
+            const v3f v = s.integ->rgb->data[p];
+            if (v.x != 0.f || v.y != 0.f || v.z != 0.f) {
+                if (n < 16) sp.push_back(i2f(p)), sp.push_back(v.x), sp.push_back(v.y), sp.push_back(v.z);
+                n++;
+            }
+        }
+        out.push_back(i2f(n));
+        sp.resize(64, 0.f);
+        out.insert(out.end(), sp.begin(), sp.end());
+    }
+    writeBin(argv[8], out.data(), out.size() * 4);
+    printf("{\"records\": %zu}\n", out.size() / (3 + 625 + 1 + 64));
+    (void)argv[9];
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -369,6 +553,8 @@ int main(int argc, char** argv) {
     if (cmd == "dump" && argc >= 6) return cmdDump(argc, argv);
     if (cmd == "exr") return cmdExr(argc, argv);
     if (cmd == "toml") return cmdToml(argc, argv);
+    if (cmd == "kat") return cmdKat(argc, argv);
+    if (cmd == "sample_state") return cmdSampleState(argc, argv);
     fprintf(stderr, "bad command\n");
     return 2;
 }

@@ -121,3 +121,22 @@ def test_ingest_matches_oracle_on_generated_scenes(gen, tmp_path):
     info = s.info()
     assert info["shapes"] == (7008 if gen == "many_shapes_obj" else 9)
     assert info["emitters"] == 1
+
+
+def test_sampler_state_is_std_mt19937():
+    """Sampler (math.h:63-76) state as libstdc++ streams it: the 10000th output of
+    std::mt19937(5489) is 4123659995 (the C++ standard's check value), and the
+    C-ABI's bdpt_sampler_state(seed, draws) equals the Python mirror advanced by draws."""
+    import ctypes
+
+    s = bdpt_amd.Sampler(5489)
+    for _ in range(9999):
+        s.next_u32()
+    assert s.next_u32() == 4123659995
+    for seed, draws in [(260450963, 0), (1, 2), (7, 227), (99, 624), (12345, 1000)]:
+        py = bdpt_amd.Sampler(seed)
+        for _ in range(draws):
+            py.next_u32()
+        st = np.zeros(bdpt_amd.MT19937_WORDS, np.uint32)
+        assert bdpt_amd.lib().bdpt_sampler_state(seed, draws, ctypes.c_void_p(st.ctypes.data)) == 0
+        assert np.array_equal(st, py.state), (seed, draws)
