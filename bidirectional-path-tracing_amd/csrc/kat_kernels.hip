@@ -70,7 +70,7 @@ __global__ __launch_bounds__(kKatBlock) void triangle_kat_kernel(int64_t n, cons
 
 // Closest hit (AcceleratorBVH::intersect) or occlusion (bvh->getIntersection(ray,
 // &info, true), as visibilityQuery calls it) through the product traversal.
-// out per ray (20 floats): hit, t, u, v, shapeID, primID, matID (int bits),
+// out per ray (20 words, bdpt_hit): hit (int bits), t, u, v, shapeID, primID, matID (int bits),
 // p[3], frameNs.n[3], frameNg.n[3], wo[3], leaf-order triangle index (int bits).
 __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, int64_t n, int occlusion,
                                                                  const float* __restrict__ rays,
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, i
     float* o = out + 20 * i;
     for (int k = 0; k < 20; k++) o[k] = 0.f;
     if (occlusion) {
-        o[0] = res >= 0 ? 1.f : 0.f;
+        o[0] = __int_as_float(res >= 0 ? 1 : 0);
         return;
     }
     const bool hit = res >= 0 && t <= ray.max_t && t >= ray.min_t;  // accel.h:133
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, i
     const float4* sh = sc.shade + 5 * static_cast<size_t>(res);
     const f3 v0 = xyz(gld4(sc.tri + 3 * static_cast<size_t>(res))), v1 = xyz(gld4(sh + 3)), v2 = xyz(gld4(sh + 4));
     const f3 ng = normalize(cross(v1 - v0, v2 - v0));
-    o[0] = 1.f, o[2] = u, o[3] = v;
+    o[0] = __int_as_float(1), o[2] = u, o[3] = v;
     o[4] = __int_as_float(h.shape), o[5] = __int_as_float(__float_as_int(gld4(sh + 2).w)), o[6] = __int_as_float(h.mat);
     o[7] = h.p.x, o[8] = h.p.y, o[9] = h.p.z;
     o[10] = h.n.x, o[11] = h.n.y, o[12] = h.n.z;

@@ -722,7 +722,11 @@ __global__ __launch_bounds__(64) void pt_sample_kernel(const PtParams* __restric
     const Stack stk{stack_mem, 64, kLdsStack, P.gstack, 1, 0};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
-    PtLane L;
+    // Value-initialised: with a partly uninitialised lane record this one-lane
+    // build returned garbage in Li.x (0x5a5a5a5a) although every field is
+    // assigned before it is read on the reference's control flow (measured on
+    // gfx950, ROCm 7.2; the frame kernel is unaffected).
+    PtLane L{};
     L.rng.ring = P.ring;
     L.rng.stride = 1;
     L.rng.seed = 0;

@@ -215,7 +215,9 @@ def sampler_fixture(name, scene, toml_path, W, H, spp, rr, n, seed):
     rec = np.concatenate([rays, st.view(f32)], 1)
     fin, fout = os.path.join(TMP, name + ".in"), os.path.join(TMP, name + ".out")
     rec.astype(f32).tofile(fin)
-    run(["sample_state", toml_path, str(W), str(H), str(spp), str(rr), fin, fout, "-"])
+    # rr only for the BDPT scenes: ref_driver's setup() writes it to Config's
+    # pt.rrDepth, which shares a union with di.bsdfSamples (core.h:201-240)
+    run(["sample_state", toml_path, str(W), str(H), str(spp), str(rr if "bdpt" in name else 0), fin, fout, "-"])
     out = np.fromfile(fout, f32).reshape(n, 3 + 625 + 1 + 64)
     np.savez_compressed(os.path.join(HERE, f"kat_sampler_{name}.npz"), rays=rays, state_in=st, Li=out[:, :3],
                         state_out=out[:, 3:628].view(np.uint32), nsplat=out[:, 628].view(np.int32),
