@@ -101,6 +101,15 @@ def _ai32(a):
     return np.ascontiguousarray(np.asarray(a, np.int32).reshape(-1))
 
 
+MAX_DEVICES = 16  # BDPT_MAX_DEVICES
+
+
+class _MultiStats(ctypes.Structure):  # bdpt_multi_stats
+    _fields_ = [("devices", ctypes.c_int32), ("rccl", ctypes.c_int32), ("wall_ms", ctypes.c_double),
+                ("render_ms", ctypes.c_double), ("reduce_ms", ctypes.c_double), ("samples", ctypes.c_int64),
+                ("kernel_ms", ctypes.c_double * MAX_DEVICES), ("device_samples", ctypes.c_int64 * MAX_DEVICES)]
+
+
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
                 ("counters", ctypes.c_int64 * len(COUNTER_NAMES))]  # BDPT_NUM_COUNTERS
@@ -171,6 +180,11 @@ def lib():
         L.bdpt_debug_fresnel.argtypes = [i32, i64, vp, vp]
         L.bdpt_debug_triangle.argtypes = [i32, i64, vp, vp, vp]
         L.bdpt_get_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
+        L.bdpt_multi_create.argtypes = [vp, i32, vp, ctypes.POINTER(vp)]
+        L.bdpt_multi_destroy.argtypes = [vp]
+        L.bdpt_multi_render_host.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_PathParams),
+                                             ctypes.POINTER(_DirectParams), vp]
+        L.bdpt_multi_get_stats.argtypes = [vp, ctypes.POINTER(_MultiStats)]
         L.bdpt_synchronize.argtypes = [vp]
         L.bdpt_config_load_toml.argtypes = [ctypes.c_char_p, ctypes.POINTER(_Config)]
         L.bdpt_render_path.argtypes = [vp, ctypes.POINTER(_FrameParams), ctypes.POINTER(_PathParams), vp, vp]
@@ -610,6 +624,52 @@ class DirectIntegrator(BDPTIntegrator):
         p, d = self.params(row_offset, row_stride, flags), self.direct.c()
         _check(lib().bdpt_render_direct(self._h, ctypes.byref(p), ctypes.byref(d), ctypes.c_void_p(fb_ptr),
                                         ctypes.c_void_p(stream_ptr)))
+
+
+class MultiDeviceRenderer:
+    """One process, several HIP devices (bdpt_multi_*): the reference's parallel_for
+    over host threads (parallelfor.h:25-65) as one context and stream per device,
+    interleaved row shards, and one RCCL sum-reduce of the frames to devices[0].
+    A repeated device (e.g. [0, 0]) rehearses the decomposition on one GPU with a
+    local sum instead of RCCL."""
+
+    def __init__(self, scene: Scene, config: Config, devices=(0,), path: PathSettings | None = None,
+                 direct: DirectSettings | None = None):
+        self.scene, self.config, self.devices = scene, config, list(devices)
+        self.path, self.direct = path, direct
+        dev = (ctypes.c_int32 * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        _check(lib().bdpt_multi_create(scene._h, len(self.devices), dev, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.bdpt_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def render_frame(self) -> np.ndarray:
+        c = self.config
+        p = _FrameParams()
+        p.camera = c.camera.c()
+        p.width, p.height, p.spp = c.width, c.height, c.spp
+        p.rr_depth = 1 if (self.path or self.direct) else c.rr_depth  # rrDepth is the BDPT setting
+        p.strategy, p.seed_base = c.strategy, c.seed_base & 0xFFFFFFFF
+        p.row_offset, p.row_stride, p.flags = 0, 1, 0
+        rgb = np.zeros((c.height, c.width, 3), np.float32)
+        pp = ctypes.byref(self.path.c()) if self.path else None
+        dp = ctypes.byref(self.direct.c()) if self.direct else None
+        _check(lib().bdpt_multi_render_host(self._h, ctypes.byref(p), pp, dp, rgb.ctypes.data))
+        return rgb
+
+    def stats(self) -> dict:
+        s = _MultiStats()
+        _check(lib().bdpt_multi_get_stats(self._h, ctypes.byref(s)))
+        n = s.devices
+        return dict(devices=n, rccl=bool(s.rccl), wall_ms=s.wall_ms, render_ms=s.render_ms, reduce_ms=s.reduce_ms,
+                    samples=s.samples, kernel_ms=list(s.kernel_ms)[:n], device_samples=list(s.device_samples)[:n])
 
 
 def debug_math(fn: str, x: np.ndarray, y: np.ndarray | None = None, device: int = 0) -> np.ndarray:

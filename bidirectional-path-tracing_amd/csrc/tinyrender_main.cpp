@@ -9,7 +9,8 @@
 // substrate) are accepted; the other
 // integrators and the realtime render passes are rejected with an error.
 // Optional overrides (not in the reference): --width W --height H --spp N
-// --rr D --device K --out FILE.exr --seed S.
+// --rr D --device K --out FILE.exr --seed S, and --gpus N / --devices a,b,...
+// to render on several devices (row shards + one RCCL sum-reduce, bdpt_multi_*).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -41,13 +42,14 @@ std::string exr_path_of(const std::string& toml) {
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "Syntax: %s <scene.toml> [nogui] [--width W --height H --spp N --rr D --device K "
-                             "--out FILE.exr --seed S]\n", argv[0]);
+                             "--out FILE.exr --seed S --gpus N --devices a,b,...]\n", argv[0]);
         return EXIT_FAILURE;
     }
     const std::string toml = argv[1];
     int W = -1, H = -1, spp = -1, rr = -1, device = 0;
     long long seed = -1;
     std::string out;
+    std::vector<int32_t> devices;  // non-empty: the multi-device render
     for (int i = 2; i < argc; i++) {
         const std::string a = argv[i];
         auto next = [&](const char* flag) -> const char* {
@@ -65,6 +67,18 @@ int main(int argc, char** argv) {
         else if (a == "--device") device = std::atoi(next("--device"));
         else if (a == "--seed") seed = std::atoll(next("--seed"));
         else if (a == "--out") out = next("--out");
+        else if (a == "--gpus") {
+            const int n = std::atoi(next("--gpus"));
+            devices.clear();
+            for (int k = 0; k < n; k++) devices.push_back(k);
+        } else if (a == "--devices") {
+            devices.clear();
+            for (const char* q = next("--devices"); *q;) {
+                devices.push_back(static_cast<int32_t>(std::strtol(q, const_cast<char**>(&q), 10)));
+                if (*q == ',') q++;
+                else if (*q) break;
+            }
+        }
         else {
             std::fprintf(stderr, "unknown argument %s\n", a.c_str());
             return EXIT_FAILURE;
@@ -95,7 +109,13 @@ int main(int argc, char** argv) {
     bdpt_scene* scene = nullptr;
     if (bdpt_scene_load_obj(cfg.obj_file, &scene) != BDPT_OK) return die("Scene::load");
     bdpt_ctx* ctx = nullptr;
-    if (bdpt_ctx_create(scene, device, &ctx) != BDPT_OK) return die("bdpt_ctx_create");
+    bdpt_multi* multi = nullptr;
+    if (!devices.empty()) {
+        if (bdpt_multi_create(scene, static_cast<int32_t>(devices.size()), devices.data(), &multi) != BDPT_OK)
+            return die("bdpt_multi_create");
+    } else if (bdpt_ctx_create(scene, device, &ctx) != BDPT_OK) {
+        return die("bdpt_ctx_create");
+    }
 
     bdpt_frame_params p;
     std::memset(&p, 0, sizeof(p));
@@ -114,26 +134,38 @@ int main(int argc, char** argv) {
     if (path) {
         if (rr > 0) cfg.path.rr_depth = rr;
         p.rr_depth = 1;  // unused by the path tracer
-        if (bdpt_render_path_host(ctx, &p, &cfg.path, rgb.data()) != BDPT_OK) return die("bdpt_render_path_host");
+        const int rc = multi ? bdpt_multi_render_host(multi, &p, &cfg.path, nullptr, rgb.data())
+                             : bdpt_render_path_host(ctx, &p, &cfg.path, rgb.data());
+        if (rc != BDPT_OK) return die("render (path)");
     } else if (direct) {
         p.rr_depth = 1;  // unused by the direct integrator
-        if (bdpt_render_direct_host(ctx, &p, &cfg.direct, rgb.data()) != BDPT_OK) {
+        const int rc = multi ? bdpt_multi_render_host(multi, &p, nullptr, &cfg.direct, rgb.data())
+                             : bdpt_render_direct_host(ctx, &p, &cfg.direct, rgb.data());
+        if (rc != BDPT_OK) {
             if (cfg.direct.sampling_strategy == 0) {  // direct.h:460-461
                 std::printf("Error: wrong strategy\n");
                 return EXIT_FAILURE;
             }
-            return die("bdpt_render_direct_host");
+            return die("render (direct)");
         }
-    } else if (bdpt_render_host(ctx, &p, rgb.data()) != BDPT_OK) {
-        return die("bdpt_render_host");
+    } else if ((multi ? bdpt_multi_render_host(multi, &p, nullptr, nullptr, rgb.data())
+                      : bdpt_render_host(ctx, &p, rgb.data())) != BDPT_OK) {
+        return die("render (bdpt)");
     }
     const auto t1 = std::chrono::high_resolution_clock::now();
     std::printf("Render took: %g seconds.\n", std::chrono::duration<double>(t1 - t0).count());
+    if (multi) {
+        bdpt_multi_stats st;
+        bdpt_multi_get_stats(multi, &st);
+        std::printf("%d devices (%s): render %.3f ms, reduce %.3f ms\n", st.devices, st.rccl ? "RCCL reduce" : "local sum",
+                    st.render_ms, st.reduce_ms);
+    }
 
     const std::string exr = out.empty() ? exr_path_of(toml) : out;
     if (bdpt_save_exr(rgb.data(), cfg.width, cfg.height, exr.c_str()) != BDPT_OK) return die("saveEXR");
     std::printf("\nSaved EXR image to %s\n", exr.c_str());  // utils.h:149
-    bdpt_ctx_destroy(ctx);
+    if (multi) bdpt_multi_destroy(multi);
+    if (ctx) bdpt_ctx_destroy(ctx);
     bdpt_scene_free(scene);
     return EXIT_SUCCESS;
 }

@@ -245,6 +245,36 @@ int bdpt_render_direct_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, co
 /* samplingStrategy string -> BDPT_DIRECT_* (0 when unknown). */
 int32_t bdpt_direct_strategy(const char* name);
 
+/* ---- several HIP devices in one process ---- */
+/* The reference fans the offline loop out over host threads (parallel_for,
+ * src/core/parallelfor.h:25-65, renderer.cpp:157); here every device gets one
+ * context, one stream and one full-frame buffer. Device i renders the
+ * interleaved row shard i, i + N, ... of the image; one RCCL sum-reduce
+ * (ncclReduce over communicators from ncclCommInitAll, librccl loaded at first
+ * use) brings the frames to devices[0]. A device list naming one device more than
+ * once (a single-GPU rehearsal) sums on that device without RCCL. */
+#define BDPT_MAX_DEVICES 16
+typedef struct bdpt_multi bdpt_multi;
+typedef struct {
+    int32_t devices;   /* N */
+    int32_t rccl;      /* 1: the reduce ran over RCCL */
+    double wall_ms;    /* host wall time of the last bdpt_multi_render_host */
+    double render_ms;  /* root-device events: start .. every device's render done */
+    double reduce_ms;  /* root-device events: the reduce */
+    int64_t samples;   /* camera samples over all devices */
+    double kernel_ms[BDPT_MAX_DEVICES];      /* per device, HIP events of its render kernel */
+    int64_t device_samples[BDPT_MAX_DEVICES];
+} bdpt_multi_stats;
+int bdpt_multi_create(const bdpt_scene* scene, int32_t ndevices, const int32_t* devices, bdpt_multi** out);
+int bdpt_multi_destroy(bdpt_multi* multi);
+/* The whole image (params->row_offset 0, row_stride 1) over all devices; the frame
+ * is ADDED to fb_host (W*H*3 floats) as bdpt_render_host does. path / direct:
+ * NULL for BDPT, else the PathTracerIntegrator / DirectIntegrator settings (at most
+ * one). Synchronous. */
+int bdpt_multi_render_host(bdpt_multi* multi, const bdpt_frame_params* params, const bdpt_path_params* path,
+                           const bdpt_direct_params* direct, float* fb_host);
+int bdpt_multi_get_stats(bdpt_multi* multi, bdpt_multi_stats* out);
+
 /* ---- the BSDF plugin contract and the path's building blocks, batched on the device ---- */
 /* All arrays are host arrays of n elements; directions are in the local shading
  * frame (z = the shading normal) as SurfaceInteraction::wo / wi. Synchronous. */
