@@ -62,7 +62,7 @@ class _FrameParams(ctypes.Structure):
 class _SceneInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in
                 ("triangles", "bvh_nodes", "shapes", "materials", "emitters", "bvh_max_depth", "device_bytes",
-                 "bvh_leaves", "wide_nodes", "wide_depth", "wide_max_stack")]
+                 "bvh_leaves", "wide_nodes", "wide_depth", "wide_max_stack", "wide_leaves", "triangle_tree")]
 
 
 class _PathParams(ctypes.Structure):  # bdpt_path_params

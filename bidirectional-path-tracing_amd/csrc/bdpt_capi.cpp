@@ -219,8 +219,10 @@ int bdpt_scene_get_info(const bdpt_scene* s, bdpt_scene_info* out) {
     out->wide_nodes = static_cast<int64_t>(L.wnodes.size() / 8);
     out->wide_depth = L.wdepth;
     out->wide_max_stack = L.wmax_stack;
+    out->wide_leaves = L.wleaves;
+    out->triangle_tree = L.tri_tree ? 1 : 0;
     out->device_bytes = static_cast<int64_t>((L.tri.size() + L.shade.size() + L.nodes.size() + L.wnodes.size() +
-                                              L.emit_tri.size()) * 16 +
+                                              L.wtri.size() + L.lbox.size() + L.emit_tri.size()) * 16 +
                                              L.bsdfs.size() * sizeof(BsdfRecord) +
                                              L.emitters.size() * sizeof(EmitterRecord) + L.emit_cdf.size() * 4 +
                                              L.shape_emitter.size() * 4);
@@ -334,6 +336,10 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     if ((rc = upload(c.get(), L.wnodes.data(), L.wnodes.size() * 16, &p))) return rc;
     c->sc.wnodes = static_cast<const float4*>(p);
     c->sc.wroot_link = L.wroot_link;
+    if ((rc = upload(c.get(), L.wtri.data(), L.wtri.size() * 16, &p))) return rc;
+    c->sc.wtri = static_cast<const float4*>(p);
+    if ((rc = upload(c.get(), L.lbox.data(), L.lbox.size() * 16, &p))) return rc;
+    c->sc.lbox = static_cast<const float4*>(p);
     if ((rc = upload(c.get(), L.bsdfs.data(), L.bsdfs.size() * sizeof(BsdfRecord), &p))) return rc;
     c->sc.bsdf = static_cast<const BsdfRecord*>(p);
     if ((rc = upload(c.get(), L.emitters.data(), L.emitters.size() * sizeof(EmitterRecord), &p))) return rc;

@@ -41,7 +41,9 @@ struct DevScene {
     const float4* __restrict__ tri;
     const float4* __restrict__ shade;
     const float4* __restrict__ nodes;   // the reference's binary tree (2 child boxes per record)
-    const float4* __restrict__ wnodes;  // 4-wide nodes over the same leaves (wide_bvh.hpp)
+    const float4* __restrict__ wnodes;  // 4-wide traversal nodes (wide_bvh.hpp)
+    const float4* __restrict__ wtri;    // traversal triangles, that tree's leaf order (v0|ref index, e1|ref leaf, e2)
+    const float4* __restrict__ lbox;    // exact box of every reference leaf (lo, hi)
     const BsdfRecord* __restrict__ bsdf;
     const EmitterRecord* __restrict__ emit;
     const float4* __restrict__ emit_tri;
@@ -570,7 +572,9 @@ __device__ __forceinline__ bool first_active_lane() {
 
 // Triangle tests of one reference leaf (bvh.h:291-309). Closest: keeps the
 // minimum t, ties to the lowest index (the reference's strict `<` in its
-// left-first DFS = leaf order). Any: true on a hit inside [min_t, max_t].
+// left-first DFS = leaf order). Any: true on a hit with t <= max_t — the
+// reference's occlusion query returns at a hit inside [min_t, max_t] and
+// otherwise reports any hit closer than max_t it kept (bvh.h:298-305, :350).
 // The triangles are fetched BDPT_LEAF_GROUP at a time with all their loads in
 // flight together (one memory round trip per group instead of two per
 // triangle); indices past the leaf's count are clamped and their results unused.
@@ -629,7 +633,7 @@ __device__ __forceinline__ bool leaf_tests(const float4* __restrict__ tri, uint3
             if (COUNT) tri_count++;
             if (tri_test_edges(xyz(q[g][0]), xyz(q[g][1]), xyz(q[g][2]), r, t, u, v)) {
                 if (any) {
-                    if (t <= r.max_t && t >= r.min_t) {
+                    if (t <= r.max_t) {
                         best = 1;
                         return true;
                     }
@@ -699,18 +703,19 @@ __device__ __forceinline__ int child_fast(float lx, float hx, float ly, float hy
 
 // Closest-hit / occlusion query over the 4-wide hierarchy (wide_bvh.hpp),
 // written as a resumable step so persistent kernels can refill finished lanes.
-// Interior children: a conservative test (ambiguous counts as a hit) — any box
-// containing a reachable leaf box passes the reference's test, so it is never
-// rejected. Leaf children (the reference's leaves): decided exactly (fast
-// test, then the cross pairs, then the reference's own divisions). Children
-// are visited near-first; stacked entries carry their entry distance and are
+// Every child box is tested conservatively (an ambiguous fast test counts as a
+// hit): the boxes bound the (padded) triangles below them. Whether a triangle
+// is a candidate of the reference's search at all is decided per triangle hit,
+// by the exact test of its reference leaf box (wleaf_tests). Children are
+// visited near-first; stacked entries carry their entry distance and are
 // dropped on pop once a closer hit exists.
 // The scene pointers a walk needs, copied once per query into registers: the
 // DevScene lives in a parameter block in global memory, and reading a field
 // through it inside the node loop would put a dependent load in front of
 // every node fetch (the compiler must assume the block may change).
 struct TravScene {
-    const float4* __restrict__ tri;
+    const float4* __restrict__ wtri;
+    const float4* __restrict__ lbox;
     const float4* __restrict__ wnodes;
     uint32_t wroot_link;
 };
@@ -721,8 +726,50 @@ __device__ __forceinline__ const float4* uniform_ptr(const float4* p) {
     return reinterpret_cast<const float4*>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 __device__ __forceinline__ TravScene trav_scene(const DevScene& sc) {
-    return TravScene{uniform_ptr(sc.tri), uniform_ptr(sc.wnodes),
+    return TravScene{uniform_ptr(sc.wtri), uniform_ptr(sc.lbox), uniform_ptr(sc.wnodes),
                      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sc.wroot_link)))};
+}
+
+// Triangle tests of one traversal leaf (wtri records). A hit is a candidate of
+// the reference's search iff the triangle's reference leaf box passes
+// BBox::intersect (bvh.h:33-69; wide_bvh.hpp) — checked exactly (fast test,
+// cross pairs, the reference's divisions) and only for a hit that would become
+// the closest (minimum t, ties to the lowest reference index = the reference's
+// strict `<` in its left-first DFS) or that ends an occlusion query (t <= max_t,
+// see leaf_tests).
+template <bool COUNT>
+__device__ __forceinline__ bool ref_leaf_passes(const float4* __restrict__ lbox, uint32_t leaf, const Ray& r,
+                                                const RayInv& ri, Counts& cnt) {
+    const float4 lo = gld4(lbox + 2 * static_cast<size_t>(leaf)), hi = gld4(lbox + 2 * static_cast<size_t>(leaf) + 1);
+    float tn, tf;
+    uint32_t fb = 0;
+    const bool pass = box_test<COUNT>(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, r, ri, tn, tf, fb);
+    if (COUNT) cnt.c[15] += fb;
+    return pass;
+}
+template <bool COUNT>
+__device__ __forceinline__ bool wleaf_tests(const float4* __restrict__ wtri, const float4* __restrict__ lbox,
+                                            uint32_t link, const Ray& r, const RayInv& ri, bool any, float& best_t,
+                                            int& best, float& best_u, float& best_v, Counts& cnt) {
+    const uint32_t start = (link >> 3) & 0x0fffffffu, count = link & 7u;
+    for (uint32_t k = 0; k < count; k++) {
+        const size_t i = static_cast<size_t>(start + k);
+        const float4 q0 = gld4(wtri + 3 * i), q1 = gld4(wtri + 3 * i + 1), q2 = gld4(wtri + 3 * i + 2);
+        float t, u, v;
+        if (COUNT) cnt.c[3]++;
+        if (!tri_test_edges(xyz(q0), xyz(q1), xyz(q2), r, t, u, v)) continue;
+        const int idx = __float_as_int(q0.w);
+        if (any) {
+            if (t <= r.max_t && ref_leaf_passes<COUNT>(lbox, __float_as_uint(q1.w), r, ri, cnt)) {
+                best = idx;
+                return true;
+            }
+        } else if ((t < best_t || (t == best_t && best >= 0 && idx < best)) &&
+                   ref_leaf_passes<COUNT>(lbox, __float_as_uint(q1.w), r, ri, cnt)) {
+            best_t = t, best = idx, best_u = u, best_v = v;
+        }
+    }
+    return false;
 }
 
 struct TravState {
@@ -770,16 +817,7 @@ __device__ __forceinline__ bool trav_node(const TravScene& sc, const Ray& r, con
                     chz = (&hz.x)[c];
         const uint32_t l = __float_as_uint((&lk.x)[c]);
         float tn, tf;
-        int d = slab_fast(clx, cly, clz, chx, chy, chz, r.o, ri.inv, tn, tf);
-        const bool leaf = (l & kLeafBit) != 0 && l != kEmptyLinkDev;
-        if (d == kSlabAmbiguous && leaf) {
-            d = slab_cross(clx, cly, clz, chx, chy, chz, r.o, ri.inv);
-            if (d == kSlabAmbiguous) {
-                if (COUNT) cnt.c[15]++;
-                float en, ex;
-                d = slab(clx, cly, clz, chx, chy, chz, r, en, ex) ? kSlabHit : kSlabMiss;
-            }
-        }
+        const int d = slab_fast(clx, cly, clz, chx, chy, chz, r.o, ri.inv, tn, tf);
         const bool hit = l != kEmptyLinkDev && d != kSlabMiss && !(tn > far) && !(tf < kCullNear);
         key[c] = hit ? tn : __builtin_inff();
         lnk[c] = hit ? l : kEmptyLinkDev;
@@ -817,7 +855,8 @@ __device__ __forceinline__ bool trav_step(const TravScene& sc, const Ray& r, con
         if (first_active_lane()) cnt.c[9]++;
     }
     if (ts.link & kLeafBit) {
-        if (leaf_tests<COUNT>(sc.tri, ts.link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return true;
+        if (wleaf_tests<COUNT>(sc.wtri, sc.lbox, ts.link, r, ri, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt))
+            return true;
     } else if (trav_node<COUNT>(sc, r, ri, any, ts, stk, cnt)) {
         return false;
     }
@@ -847,7 +886,8 @@ __device__ __forceinline__ void trav_while_while(const TravScene& sc, const Ray&
             cnt.c[8]++;
             if (first_active_lane()) cnt.c[9]++;
         }
-        if (leaf_tests<COUNT>(sc.tri, ts.link, r, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt.c[3])) return;
+        if (wleaf_tests<COUNT>(sc.wtri, sc.lbox, ts.link, r, ri, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt))
+            return;
         if (!trav_pop(r, any, ts, stk)) return;
     }
 }

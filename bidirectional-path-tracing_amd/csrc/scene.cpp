@@ -649,12 +649,49 @@ bool build_device_layout(const HostScene& s, DeviceLayout& out, std::string& err
         r[3] = {bits(static_cast<int32_t>(link_of(i + 1))), bits(static_cast<int32_t>(link_of(i + s.nodes[i].right_offset))),
                 0.f, 0.f};
     }
-    WideBvh wb;
-    if (!build_wide_bvh(s.nodes, wb, err)) return false;
-    out.wnodes.swap(wb.nodes);
-    out.wroot_link = wb.root_link;
-    out.wmax_stack = wb.max_stack;
-    out.wdepth = wb.depth;
+    // Traversal hierarchy (wide_bvh.hpp): by default a 4-wide SAH tree over single
+    // triangles; BDPT_TRAV_TREE=refleaf keeps the reference's leaves as its leaves
+    // (the round-1 layout, for comparisons). Both feed the same device code.
+    const char* tree_env = std::getenv("BDPT_TRAV_TREE");
+    out.tri_tree = !(tree_env && std::string(tree_env) == "refleaf");
+    if (out.tri_tree) {
+        TriWideBvh tb;
+        if (!build_wide_bvh_tris(s.nodes, out.tri, out.shade, kTriBoxPad, tb, err)) return false;
+        out.wnodes.swap(tb.bvh.nodes);
+        out.wroot_link = tb.bvh.root_link;
+        out.wmax_stack = tb.bvh.max_stack;
+        out.wdepth = tb.bvh.depth;
+        out.wleaves = tb.bvh.leaves;
+        out.wtri.swap(tb.tri);
+        out.lbox.swap(tb.leaf_box);
+    } else {
+        WideBvh wb;
+        if (!build_wide_bvh(s.nodes, wb, err)) return false;
+        out.wnodes.swap(wb.nodes);
+        out.wroot_link = wb.root_link;
+        out.wmax_stack = wb.max_stack;
+        out.wdepth = wb.depth;
+        out.wleaves = wb.leaves;
+        out.wtri.resize(3 * n);
+        int32_t leaf_id = 0;
+        for (const FlatNode& f : s.nodes) {
+            if (f.right_offset != 0) continue;
+            for (uint32_t k = 0; k < f.nprims; k++) {
+                const size_t i = f.start + k;
+                out.wtri[3 * i] = {out.tri[3 * i].x, out.tri[3 * i].y, out.tri[3 * i].z, bits(static_cast<int32_t>(i))};
+                out.wtri[3 * i + 1] = {out.tri[3 * i + 1].x, out.tri[3 * i + 1].y, out.tri[3 * i + 1].z, bits(leaf_id)};
+                out.wtri[3 * i + 2] = out.tri[3 * i + 2];
+            }
+            out.lbox.push_back({f.bmin[0], f.bmin[1], f.bmin[2], 0.f});
+            out.lbox.push_back({f.bmax[0], f.bmax[1], f.bmax[2], 0.f});
+            leaf_id++;
+        }
+        if (s.nodes[0].right_offset == 0) {
+            const float inf = __builtin_inff();
+            out.lbox[0] = {-inf, -inf, -inf, 0.f};
+            out.lbox[1] = {inf, inf, inf, 0.f};
+        }
+    }
     out.bsdfs = s.bsdfs;
     for (const Emitter& e : s.emitters) {
         EmitterRecord r{};

@@ -66,9 +66,13 @@ struct DeviceLayout {
     std::vector<float4_t> shade;    // 5 per triangle, BVH leaf order
     std::vector<float4_t> nodes;    // 4 per interior node (the reference's binary tree)
     uint32_t root_link = 0;
-    std::vector<float4_t> wnodes;   // 8 per 4-wide node over the same leaves (wide_bvh.hpp)
+    std::vector<float4_t> wnodes;   // 8 per 4-wide traversal node (wide_bvh.hpp)
     uint32_t wroot_link = 0;
     int wmax_stack = 0, wdepth = 0;
+    int64_t wleaves = 0;
+    std::vector<float4_t> wtri;     // 3 per triangle in the traversal tree's leaf order (wide_bvh.hpp)
+    std::vector<float4_t> lbox;     // 2 per reference leaf: its exact box
+    bool tri_tree = true;           // false: traversal leaves = the reference leaves (BDPT_TRAV_TREE=refleaf)
     std::vector<BsdfRecord> bsdfs;
     std::vector<EmitterRecord> emitters;
     std::vector<float4_t> emit_tri; // 5 per emitter face, shape face order

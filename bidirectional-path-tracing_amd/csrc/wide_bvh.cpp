@@ -2,6 +2,7 @@
 #include "wide_bvh.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <functional>
 
@@ -34,7 +35,8 @@ struct Leaf {
 struct BNode {  // binary build node
     Box box;
     int left = -1, right = -1;  // children (binary node ids), -1 for a leaf
-    int leaf = -1;              // index into leaves when a leaf
+    int leaf = -1;              // index into leaves when a leaf (first of `count` consecutive ones)
+    int count = 1;
 };
 
 constexpr int kBins = 32;
@@ -46,6 +48,10 @@ class Builder {
     std::vector<BNode> nodes;
     int max_depth = 0;
     bool median_only = false;
+    // Leaves of up to max_leaf items, closed by the SAH (leaf cost n * area vs
+    // kNodeCost * area + the best split); max_leaf 1 = one item per leaf.
+    int max_leaf = 1;
+    static constexpr double kNodeCost = 1.0;
 
     int build(int b, int e, int depth) {
         max_depth = std::max(max_depth, depth);
@@ -59,7 +65,13 @@ class Builder {
             nodes[id].leaf = b;
             return id;
         }
-        const int mid = split(b, e);
+        double split_cost = 0.0;
+        const int mid = split(b, e, &split_cost);
+        if (e - b <= max_leaf && box.area() * (e - b) <= kNodeCost * box.area() + split_cost) {
+            nodes[id].leaf = b;
+            nodes[id].count = e - b;
+            return id;
+        }
         const int l = build(b, mid, depth + 1);
         const int r = build(mid, e, depth + 1);
         nodes[id].left = l;
@@ -77,7 +89,7 @@ class Builder {
         return mid;
     }
 
-    int split(int b, int e) {
+    int split(int b, int e, double* cost_out = nullptr) {
         float cl[3], ch[3];
         for (int a = 0; a < 3; a++) cl[a] = __builtin_inff(), ch[a] = -__builtin_inff();
         for (int i = b; i < e; i++)
@@ -85,6 +97,7 @@ class Builder {
         int wide_axis = 0;
         for (int a = 1; a < 3; a++)
             if (ch[a] - cl[a] > ch[wide_axis] - cl[wide_axis]) wide_axis = a;
+        if (cost_out) *cost_out = __builtin_inf();
         if (median_only || !(ch[wide_axis] > cl[wide_axis])) return median(b, e, wide_axis);
         double best = __builtin_inf();
         int best_axis = -1, best_bin = -1;
@@ -122,6 +135,7 @@ class Builder {
             }
         }
         if (best_axis < 0) return median(b, e, wide_axis);
+        if (cost_out) *cost_out = best;
         const double scale = kBins / (double(ch[best_axis]) - cl[best_axis]);
         const float lo = cl[best_axis];
         auto it = std::partition(L.begin() + b, L.begin() + e, [&](const Leaf& x) {
@@ -139,6 +153,54 @@ float u2f(uint32_t u) {
     float f;
     std::memcpy(&f, &u, 4);
     return f;
+}
+
+// Collapses the binary tree to 4-wide nodes (repeatedly opening the interior
+// child of largest area) into out.nodes; returns the root link.
+uint32_t collapse(const std::vector<BNode>& bn, const std::function<uint32_t(const BNode&)>& leaf_link, WideBvh& out) {
+    int max_stack = 0, max_depth = 0;
+    std::function<uint32_t(int, int, int)> emit = [&](int id, int depth, int stack_above) -> uint32_t {
+        std::vector<int> ch = {bn[id].left, bn[id].right};
+        while (static_cast<int>(ch.size()) < kWideArity) {
+            int pick = -1;
+            double area = -1.0;
+            for (int k = 0; k < static_cast<int>(ch.size()); k++)
+                if (bn[ch[k]].leaf < 0 && bn[ch[k]].box.area() > area) area = bn[ch[k]].box.area(), pick = k;
+            if (pick < 0) break;
+            const int c = ch[pick];
+            ch[pick] = bn[c].left;
+            ch.push_back(bn[c].right);
+        }
+        const uint32_t me = static_cast<uint32_t>(out.nodes.size() / 8);
+        out.nodes.resize(out.nodes.size() + 8);
+        max_depth = std::max(max_depth, depth + 1);
+        const int stack_here = stack_above + static_cast<int>(ch.size()) - 1;
+        max_stack = std::max(max_stack, stack_here);
+        uint32_t links[kWideArity];
+        Box boxes[kWideArity];
+        for (int k = 0; k < kWideArity; k++) {
+            if (k >= static_cast<int>(ch.size())) {
+                links[k] = kEmptyLink;
+                for (int a = 0; a < 3; a++) boxes[k].lo[a] = boxes[k].hi[a] = 0.f;
+                continue;
+            }
+            const BNode& c = bn[ch[k]];
+            boxes[k] = c.box;
+            links[k] = c.leaf >= 0 ? leaf_link(c) : emit(ch[k], depth + 1, stack_here);
+        }
+        float4_t* r = &out.nodes[8 * static_cast<size_t>(me)];
+        for (int a = 0; a < 3; a++) {
+            r[2 * a] = {boxes[0].lo[a], boxes[1].lo[a], boxes[2].lo[a], boxes[3].lo[a]};
+            r[2 * a + 1] = {boxes[0].hi[a], boxes[1].hi[a], boxes[2].hi[a], boxes[3].hi[a]};
+        }
+        r[6] = {u2f(links[0]), u2f(links[1]), u2f(links[2]), u2f(links[3])};
+        r[7] = {0.f, 0.f, 0.f, 0.f};
+        return me;
+    };
+    const uint32_t root = emit(0, 0, 0);
+    out.max_stack = max_stack;
+    out.depth = max_depth;
+    return root;
 }
 
 }  // namespace
@@ -175,52 +237,96 @@ bool build_wide_bvh(const std::vector<FlatNode>& flat, WideBvh& out, std::string
         B.nodes.swap(M.nodes);
         B.max_depth = M.max_depth;
     }
-    const std::vector<BNode>& bn = B.nodes;
-
-    // Collapse to 4-wide: repeatedly open the interior child of largest area.
-    int max_stack = 0, max_depth = 0;
-    std::function<uint32_t(int, int, int)> emit = [&](int id, int depth, int stack_above) -> uint32_t {
-        std::vector<int> ch = {bn[id].left, bn[id].right};
-        while (static_cast<int>(ch.size()) < kWideArity) {
-            int pick = -1;
-            double area = -1.0;
-            for (int k = 0; k < static_cast<int>(ch.size()); k++)
-                if (bn[ch[k]].leaf < 0 && bn[ch[k]].box.area() > area) area = bn[ch[k]].box.area(), pick = k;
-            if (pick < 0) break;
-            const int c = ch[pick];
-            ch[pick] = bn[c].left;
-            ch.push_back(bn[c].right);
-        }
-        const uint32_t me = static_cast<uint32_t>(out.nodes.size() / 8);
-        out.nodes.resize(out.nodes.size() + 8);
-        max_depth = std::max(max_depth, depth + 1);
-        const int stack_here = stack_above + static_cast<int>(ch.size()) - 1;
-        max_stack = std::max(max_stack, stack_here);
-        uint32_t links[kWideArity];
-        Box boxes[kWideArity];
-        for (int k = 0; k < kWideArity; k++) {
-            if (k >= static_cast<int>(ch.size())) {
-                links[k] = kEmptyLink;
-                for (int a = 0; a < 3; a++) boxes[k].lo[a] = boxes[k].hi[a] = 0.f;
-                continue;
-            }
-            const BNode& c = bn[ch[k]];
-            boxes[k] = c.box;
-            links[k] = c.leaf >= 0 ? leaves[c.leaf].link : emit(ch[k], depth + 1, stack_here);
-        }
-        float4_t* r = &out.nodes[8 * static_cast<size_t>(me)];
-        for (int a = 0; a < 3; a++) {
-            r[2 * a] = {boxes[0].lo[a], boxes[1].lo[a], boxes[2].lo[a], boxes[3].lo[a]};
-            r[2 * a + 1] = {boxes[0].hi[a], boxes[1].hi[a], boxes[2].hi[a], boxes[3].hi[a]};
-        }
-        r[6] = {u2f(links[0]), u2f(links[1]), u2f(links[2]), u2f(links[3])};
-        r[7] = {0.f, 0.f, 0.f, 0.f};
-        return me;
-    };
-    out.root_link = emit(0, 0, 0);
-    out.max_stack = max_stack;
-    out.depth = max_depth;
+    out.root_link = collapse(B.nodes, [&](const BNode& c) { return leaves[c.leaf].link; }, out);
     if (out.root_link != 0) {
+        err = "wide BVH root must be node 0";
+        return false;
+    }
+    return true;
+}
+
+bool build_wide_bvh_tris(const std::vector<FlatNode>& flat, const std::vector<float4_t>& tri,
+                         const std::vector<float4_t>& shade, float pad_rel, TriWideBvh& out, std::string& err) {
+    out = TriWideBvh();
+    const size_t n = tri.size() / 3;
+    if (flat.empty() || n == 0) {
+        err = "empty BVH";
+        return false;
+    }
+    // reference leaf of every triangle (leaf order) and the leaf boxes
+    std::vector<int32_t> leaf_of(n, -1);
+    for (const FlatNode& f : flat) {
+        if (f.right_offset != 0) continue;
+        const int32_t id = static_cast<int32_t>(out.leaf_box.size() / 2);
+        for (uint32_t k = 0; k < f.nprims; k++) leaf_of[f.start + k] = id;
+        out.leaf_box.push_back({f.bmin[0], f.bmin[1], f.bmin[2], 0.f});
+        out.leaf_box.push_back({f.bmax[0], f.bmax[1], f.bmax[2], 0.f});
+    }
+    if (flat[0].right_offset == 0) {  // the whole scene is one leaf: the reference tests no box
+        const float inf = __builtin_inff();
+        out.leaf_box[0] = {-inf, -inf, -inf, 0.f};
+        out.leaf_box[1] = {inf, inf, inf, 0.f};
+    }
+    std::vector<Leaf> items(n);
+    Box scene;
+    scene.clear();
+    for (size_t i = 0; i < n; i++) {
+        if (leaf_of[i] < 0) {
+            err = "triangle outside every BVH leaf";
+            return false;
+        }
+        const float4_t& v0 = tri[3 * i];
+        const float4_t& v1 = shade[5 * i + 3];
+        const float4_t& v2 = shade[5 * i + 4];
+        Box& b = items[i].box;
+        b.lo[0] = std::min({v0.x, v1.x, v2.x}), b.hi[0] = std::max({v0.x, v1.x, v2.x});
+        b.lo[1] = std::min({v0.y, v1.y, v2.y}), b.hi[1] = std::max({v0.y, v1.y, v2.y});
+        b.lo[2] = std::min({v0.z, v1.z, v2.z}), b.hi[2] = std::max({v0.z, v1.z, v2.z});
+        scene.grow(b);
+        items[i].link = static_cast<uint32_t>(i);
+    }
+    double diag = 0.0;
+    for (int a = 0; a < 3; a++) diag += (double(scene.hi[a]) - scene.lo[a]) * (double(scene.hi[a]) - scene.lo[a]);
+    const float pad = static_cast<float>(pad_rel * std::sqrt(diag));
+    for (Leaf& it : items)
+        for (int a = 0; a < 3; a++) {
+            it.c[a] = 0.5f * (it.box.lo[a] + it.box.hi[a]);
+            it.box.lo[a] = std::nextafter(it.box.lo[a] - pad, -__builtin_inff());
+            it.box.hi[a] = std::nextafter(it.box.hi[a] + pad, __builtin_inff());
+        }
+    out.pad = pad;
+    Builder B(items);
+    B.max_leaf = kTriLeafMax;
+    B.build(0, static_cast<int>(n), 0);
+    if (B.max_depth > kMaxBinaryDepth) {
+        Builder M(items);
+        M.median_only = true;
+        M.max_leaf = kTriLeafMax;
+        M.build(0, static_cast<int>(n), 0);
+        B.nodes.swap(M.nodes);
+        B.max_depth = M.max_depth;
+    }
+    // traversal triangles in the new leaf order: v0 | ref index, e1 | ref leaf, e2
+    out.tri.resize(3 * n);
+    for (size_t k = 0; k < n; k++) {
+        const uint32_t i = items[k].link;
+        const float4_t a = tri[3 * i], b = tri[3 * i + 1], c = tri[3 * i + 2];
+        out.tri[3 * k] = {a.x, a.y, a.z, u2f(i)};
+        out.tri[3 * k + 1] = {b.x, b.y, b.z, u2f(static_cast<uint32_t>(leaf_of[i]))};
+        out.tri[3 * k + 2] = {c.x, c.y, c.z, 0.f};
+    }
+    int64_t wleaves = 0;
+    if (B.nodes[0].leaf >= 0) {  // a single leaf: no node to test
+        out.bvh.root_link = make_leaf_link(0, static_cast<uint32_t>(n));
+        out.bvh.leaves = 1;
+        return true;
+    }
+    out.bvh.root_link = collapse(B.nodes, [&](const BNode& c) {
+        wleaves++;
+        return make_leaf_link(static_cast<uint32_t>(c.leaf), static_cast<uint32_t>(c.count));
+    }, out.bvh);
+    out.bvh.leaves = wleaves;
+    if (out.bvh.root_link != 0) {
         err = "wide BVH root must be node 0";
         return false;
     }

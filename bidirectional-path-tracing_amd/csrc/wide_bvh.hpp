@@ -49,4 +49,29 @@ struct WideBvh {
 // Builds the hierarchy over the leaves of the reference's flat preorder tree.
 bool build_wide_bvh(const std::vector<FlatNode>& flat, WideBvh& out, std::string& err);
 
+// The default traversal hierarchy: a binned-SAH 4-wide tree over single
+// triangles (leaves of up to kTriLeafMax, closed by the SAH), boxes padded by
+// pad_rel x the scene diagonal. A triangle is a candidate of the reference's
+// search iff its REFERENCE leaf box passes BBox::intersect (see above: for rays
+// without a zero direction component that is independent of the tree above the
+// leaves); the device checks that box exactly, but only for a triangle hit that
+// would become the result (or end an occlusion query). Everything else — node
+// boxes, leaf grouping, order — is free, so the tree is built for speed:
+// against the reference-leaf tree it halves the walk steps and cuts triangle
+// tests ~4x on the Cornell scenes (tools/trav_sim.cpp).
+//   tri:      3 float4 per triangle in this tree's leaf order: (v0, reference
+//             index bits) (e1, reference leaf id bits) (e2, 0)
+//   leaf_box: 2 float4 per reference leaf: (lo, 0) (hi, 0) — infinite when the
+//             whole reference tree is one leaf (then no box is tested)
+constexpr int kTriLeafMax = 4;
+constexpr float kTriBoxPad = 1e-4f;  // x scene diagonal: the hit-point tolerance of the culling
+struct TriWideBvh {
+    WideBvh bvh;
+    std::vector<float4_t> tri;
+    std::vector<float4_t> leaf_box;
+    float pad = 0.f;
+};
+bool build_wide_bvh_tris(const std::vector<FlatNode>& flat, const std::vector<float4_t>& tri,
+                         const std::vector<float4_t>& shade, float pad_rel, TriWideBvh& out, std::string& err);
+
 }  // namespace bdpt

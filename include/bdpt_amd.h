@@ -83,8 +83,11 @@ typedef struct {
     int64_t triangles, bvh_nodes, shapes, materials, emitters, bvh_max_depth;
     int64_t device_bytes; /* HBM bytes of the uploaded scene arrays */
     int64_t bvh_leaves;   /* reference BVH leaves (<= 4 triangles each) */
-    int64_t wide_nodes;   /* 4-wide traversal nodes built over those leaves */
+    int64_t wide_nodes;   /* 4-wide traversal nodes */
     int64_t wide_depth, wide_max_stack;
+    int64_t wide_leaves;  /* leaves of the traversal tree */
+    int64_t triangle_tree; /* 1: SAH tree over single triangles (default); 0: over the reference
+                              leaves (environment BDPT_TRAV_TREE=refleaf at scene load) */
 } bdpt_scene_info;
 
 typedef struct {
