@@ -1,6 +1,8 @@
 #!/bin/bash
 # Builds a kernel variant of the product library: tools/build_variant.sh NAME [hipcc -D flags...]
 # -> bidirectional-path-tracing_amd/lib/libbdpt_amd_NAME.so (select with BDPT_AMD_LIB=...).
+# Rebuilds the BDPT megakernel and wavefront translation units with the flags;
+# every other object comes from the default build (run make first).
 set -e
 cd "$(dirname "$0")/../bidirectional-path-tracing_amd"
 NAME=$1; shift
@@ -10,5 +12,6 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -
 /opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/bdpt_kernels.hip -o $O/k.o &
 /opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/bdpt_wavefront.hip -o $O/w.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $O/k.o $O/w.o lib/obj/bdpt_kernels_deep.o lib/obj/pt_kernels.o lib/obj/bdpt_capi.o lib/obj/math_check.o lib/obj/scene.o lib/obj/wide_bvh.o lib/obj/toml_config.o lib/obj/exr_io.o -o lib/libbdpt_amd_$NAME.so
+OTHERS=$(ls lib/obj/*.o | grep -v -e '/bdpt_kernels.o$' -e '/bdpt_wavefront.o$' -e '/tinyrender_main.o$')
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $O/k.o $O/w.o $OTHERS -ldl -o lib/libbdpt_amd_$NAME.so
 echo lib/libbdpt_amd_$NAME.so
