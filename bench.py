@@ -183,10 +183,8 @@ def main() -> None:
                     help="bdpt = the hot path (BASELINE metric); path = the reference's PathTracerIntegrator "
                          "(path.h, cbox_bdpt_path.toml settings), direct = its DirectIntegrator (direct.h, MIS, "
                          "1 emitter + 1 BSDF sample) on the same substrate, for comparison")
-    ap.add_argument("--schedule", choices=["split", "combined", "wavefront"], default="split",
-                    help="render schedule: split = light / eye passes over batches of samples (default); "
-                         "combined = BDPT_FLAG_COMBINED, one megakernel pass per sample; wavefront = "
-                         "BDPT_FLAG_WAVEFRONT shade / trace passes")
+    ap.add_argument("--schedule", choices=["megakernel", "wavefront"], default="megakernel",
+                    help="render schedule (BDPT_FLAG_WAVEFRONT for the shade/trace passes)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the in-run parity check of the GPU row shard against the CPU reference frame")
     ap.add_argument("--profiles", default=os.path.join(REPO, "profiles"),
@@ -222,7 +220,7 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     kernel_ms = []
-    sched_flags = {"split": 0, "combined": bdpt_amd.FLAG_COMBINED, "wavefront": bdpt_amd.FLAG_WAVEFRONT}[args.schedule]
+    sched_flags = bdpt_amd.FLAG_WAVEFRONT if args.schedule == "wavefront" else 0
 
     row_offset, row_stride = bdpt_dist.row_shard(rank, world)
 

@@ -33,7 +33,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BDPT_AMD_LIB") or os.path.join(HERE, "lib", "libbdpt_amd.so")
 
 STRATEGY_BDPT, STRATEGY_LIGHT_TRACING, STRATEGY_PATH_TRACING = 0, 1, 2
-FLAG_COUNT, FLAG_FULL_TRAVERSAL, FLAG_WAVEFRONT, FLAG_COMBINED = 1, 2, 4, 8
+FLAG_COUNT, FLAG_FULL_TRAVERSAL, FLAG_WAVEFRONT = 1, 2, 4
 REFERENCE_SEED = 260450963  # renderer.cpp:155
 COUNTER_NAMES = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
                  "light_vert_reads", "splats", "rng_draws", "trav_lane_iters", "trav_wave_iters",

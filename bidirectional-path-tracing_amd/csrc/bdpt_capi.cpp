@@ -22,8 +22,7 @@
 namespace bdpt {
 hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
                         uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
-                        hipStream_t stream, void* dparams, int phase = 0, float4* park = nullptr,
-                        uint64_t batch_base = 0, uint64_t batch_n = 0, bool write_params = true);
+                        hipStream_t stream, void* dparams);
 size_t frame_params_bytes();
 // sample_state.hip: the single-sample kernels (the caller's std::mt19937 state at sc.mt_ring)
 hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float* splats, float* lvbuf, uint2* gstack,
@@ -56,8 +55,7 @@ int frame_kernel_blocks_per_cu(size_t dyn_lds);
 // bdpt_kernels_deep.hip: the same megakernel for rrDepth > 28
 hipError_t launch_frame_deep(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf,
                              uint2* gstack, uint32_t nslots, unsigned long long* work, unsigned long long* counters,
-                             int grid, hipStream_t stream, void* dparams, int phase = 0, float4* park = nullptr,
-                             uint64_t batch_base = 0, uint64_t batch_n = 0, bool write_params = true);
+                             int grid, hipStream_t stream, void* dparams);
 int frame_kernel_blocks_per_cu_deep(size_t dyn_lds);
 size_t pt_params_bytes();
 int pt_blocks_per_cu(size_t dyn_lds);
@@ -128,17 +126,7 @@ struct bdpt_ctx {
     unsigned long long* counters = nullptr;  // kCounters
     float* lv = nullptr;
     size_t lv_floats = 0;
-    // split schedule: two batch buffers (light vertices in lv, parked samples in
-    // park, 4 float4 each), a second stream for the eye passes, per-parity
-    // parameter blocks, and events light-done / eye-done per parity
-    float4* park = nullptr;
-    uint64_t park_cap = 0;  // samples per half
-    hipStream_t stream2 = nullptr;
-    uint2* gstack2 = nullptr;  // traversal-stack overflow of the eye passes (they run beside light passes)
-    void* split_params[4] = {nullptr, nullptr, nullptr, nullptr};  // (light, eye) x parity
-    hipEvent_t light_done[2] = {nullptr, nullptr}, eye_done[2] = {nullptr, nullptr}, split_start = nullptr;
     uint2* gstack = nullptr;  // traversal-stack overflow beyond the LDS part
-    size_t gstack_mega = 0;   // its entries used by one frame-kernel launch
     uint32_t nslots = 0;
     float* tmp_fb = nullptr;
     size_t tmp_fb_floats = 0;
@@ -301,14 +289,6 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
     // Teardown is best effort: errors here cannot be acted on by the caller.
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocs) (void)hipFree(p);
-    if (c->park) hipFree(c->park);
-    if (c->stream2) hipStreamSynchronize(c->stream2);
-    if (c->gstack2) hipFree(c->gstack2);
-    for (void* q : c->split_params)
-        if (q) hipFree(q);
-    for (hipEvent_t e : {c->light_done[0], c->light_done[1], c->eye_done[0], c->eye_done[1], c->split_start})
-        if (e) hipEventDestroy(e);
-    if (c->stream2) hipStreamDestroy(c->stream2);
     for (void* p : {static_cast<void*>(c->work), static_cast<void*>(c->counters), static_cast<void*>(c->lv),
                     static_cast<void*>(c->gstack), static_cast<void*>(c->wf_lane), static_cast<void*>(c->wf_ray),
                     static_cast<void*>(c->wf_res), static_cast<void*>(c->wf_wctr), static_cast<void*>(c->wf_tctr),
@@ -403,7 +383,7 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
         }
     }
     c->max_depth = s->host.max_depth;
-    HIP_TRY(hipMalloc(&c->work, 4 * sizeof(unsigned long long)));  // split schedule: (light, eye) x parity
+    HIP_TRY(hipMalloc(&c->work, sizeof(unsigned long long)));
     HIP_TRY(hipMalloc(&c->counters, sizeof(unsigned long long) * BDPT_NUM_COUNTERS));
     HIP_TRY(hipMalloc(&c->sample_out, 16 * sizeof(float)));
     HIP_TRY(hipMalloc(&c->dparams, frame_params_bytes()));
@@ -418,7 +398,6 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     c->trace_lanes = static_cast<uint32_t>(c->trace_grid * wf_trace_block());
     const int depth = std::max(s->host.max_depth + 2, L.wmax_stack + 1);
     const size_t spill_mega = static_cast<size_t>(std::max(0, depth - frame_kernel_lds_stack())) * c->nslots;
-    c->gstack_mega = spill_mega;
     const size_t spill_wf = static_cast<size_t>(std::max(0, depth - wf_trace_lds_stack())) * c->trace_lanes;
     HIP_TRY(hipMalloc(&c->gstack, sizeof(uint2) * std::max<size_t>(1, std::max(spill_mega, spill_wf))));
     c->shade_depth = s->host.max_depth + 2;
@@ -542,77 +521,6 @@ static int render_wavefront(bdpt_ctx* c, const dev::DevFrame& fr, float* fb, hip
     return BDPT_OK;
 }
 
-// Split schedule (the default for rrDepth <= 28): the shard's samples in
-// batches; per batch a light pass (primary ray + light subpath, samples parked
-// at the start of the eye subpath) then an eye pass (eye subpath + connections).
-// Batch-indexed light vertices (rrDepth - 1 records) and a 64-byte parked record
-// per sample, two batches resident: BDPT_SPLIT_BATCH overrides the default of
-// 2 GiB per batch.
-static uint64_t split_batch(const bdpt_ctx* c, const dev::DevFrame& fr) {
-    const uint64_t per_sample = static_cast<uint64_t>(std::max(fr.rr_depth - 1, 1)) * 64 + 64;
-    uint64_t cap = (2ull << 30) / per_sample;
-    if (const char* e = std::getenv("BDPT_SPLIT_BATCH")) {
-        const long long v = std::atoll(e);
-        if (v >= 1) cap = static_cast<uint64_t>(v);
-    }
-    cap = std::max<uint64_t>(cap, 64);
-    return std::min<uint64_t>(cap, fr.total_samples);
-}
-
-static int ensure_split(bdpt_ctx* c, int rr_depth, uint64_t n) {
-    int rc;
-    if ((rc = ensure_lv(c, rr_depth, static_cast<uint32_t>(2 * n)))) return rc;
-    if (n > c->park_cap) {
-        if (c->park) HIP_TRY(hipFree(c->park));
-        c->park = nullptr;
-        HIP_TRY(hipMalloc(&c->park, sizeof(float4) * 4 * 2 * n));
-        c->park_cap = n;
-    }
-    if (!c->stream2) {
-        HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-        HIP_TRY(hipMalloc(&c->gstack2, sizeof(uint2) * std::max<size_t>(1, c->gstack_mega)));
-        for (void*& q : c->split_params) HIP_TRY(hipMalloc(&q, frame_params_bytes()));
-        for (int p = 0; p < 2; p++) {
-            HIP_TRY(hipEventCreateWithFlags(&c->light_done[p], hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&c->eye_done[p], hipEventDisableTiming));
-        }
-        HIP_TRY(hipEventCreateWithFlags(&c->split_start, hipEventDisableTiming));
-    }
-    return BDPT_OK;
-}
-
-// The split schedule's passes, software-pipelined over two streams: batch k's
-// light pass (stream st, buffer half k % 2) runs while batch k - 1's eye pass
-// (stream2) drains, so neither pass's tail idles the GPU. A half is reused
-// once the eye pass of the batch before last has finished with it.
-static int render_split(bdpt_ctx* c, const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, hipStream_t st,
-                        uint64_t batch, int64_t& launches) {
-    const size_t lv_half = static_cast<size_t>(std::max(fr.rr_depth - 1, 1)) * light_vertex_fields() * batch;
-    HIP_TRY(hipEventRecord(c->split_start, st));
-    HIP_TRY(hipStreamWaitEvent(c->stream2, c->split_start, 0));
-    uint64_t k = 0;
-    for (uint64_t b0 = 0; b0 < fr.total_samples; b0 += batch, k++) {
-        const int p = static_cast<int>(k & 1);
-        const uint64_t n = std::min<uint64_t>(batch, fr.total_samples - b0);
-        if (k >= 2) HIP_TRY(hipStreamWaitEvent(st, c->eye_done[p], 0));
-        unsigned long long* work = c->work + 2 * p;
-        float* lv = c->lv + p * lv_half;
-        float4* park = c->park + 4 * static_cast<size_t>(p) * batch;
-        HIP_TRY(hipMemsetAsync(work, 0, 2 * sizeof(unsigned long long), st));
-        HIP_TRY(launch_frame(sc, fr, fb, lv, c->gstack, c->nslots, work, c->counters, c->grid, st,
-                             c->split_params[2 * p], dev::kPhaseLight, park, b0, n, true));
-        HIP_TRY(hipEventRecord(c->light_done[p], st));
-        HIP_TRY(hipStreamWaitEvent(c->stream2, c->light_done[p], 0));
-        HIP_TRY(launch_frame(sc, fr, fb, lv, c->gstack2, c->nslots, work, c->counters, c->grid, c->stream2,
-                             c->split_params[2 * p + 1], dev::kPhaseEye, park, b0, n, true));
-        HIP_TRY(hipEventRecord(c->eye_done[p], c->stream2));
-        launches += 2;
-    }
-    // the caller's stream continues after every eye pass (stream2 runs them in order)
-    HIP_TRY(hipStreamWaitEvent(st, c->eye_done[(k - 1) & 1], 0));
-    return BDPT_OK;
-}
-
 int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_stream) {
     if (!c || !fb) return fail(BDPT_ERR_INVALID, "null argument");
     int rc = check_params(p);
@@ -621,13 +529,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const dev::DevFrame fr = make_frame(p);
     const bool mega = (p->flags & BDPT_FLAG_WAVEFRONT) == 0;
-    const bool split = mega && p->rr_depth <= kLazyRrDepth && (p->flags & BDPT_FLAG_COMBINED) == 0;
-    const uint64_t batch = split ? split_batch(c, fr) : 0;
-    if (split) {
-        if ((rc = ensure_split(c, p->rr_depth, std::max<uint64_t>(batch, 1)))) return rc;
-    } else if (mega && (rc = ensure_lv(c, p->rr_depth, c->nslots))) {
-        return rc;
-    }
+    if (mega && (rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
     dev::DevScene sc = c->sc;
     if (mega && p->rr_depth > kLazyRrDepth) {  // draws past 226: the lanes' MT19937 rings
         if (!c->mt_ring) HIP_TRY(hipMalloc(&c->mt_ring, sizeof(uint32_t) * 624 * static_cast<size_t>(c->nslots)));
@@ -640,9 +542,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     HIP_TRY(hipEventRecord(c->ev0, st));
     int64_t launches = 0;
     if (fr.total_samples > 0) {
-        if (split) {
-            if ((rc = render_split(c, sc, fr, fb, st, batch, launches))) return rc;
-        } else if (mega) {
+        if (mega) {
             if (p->rr_depth > kLazyRrDepth) {  // never more resident blocks than the slots allocated
                 const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_deep(
                                                                4 * static_cast<size_t>(c->sc.lds_words)));

@@ -18,9 +18,6 @@ constexpr float kInvTwoPi = 0.15915494309189533577f;  // platform.h:52
 constexpr float kEpsilon = 1e-8f;                     // platform.h:56
 constexpr float kTriMinT = 0x1.0624dep-10f;           // smallest float t with (double)t > 1e-3 (accel.h:43)
 constexpr int kCounters = 32;
-// Schedules of the BDPT state machine (bdpt_path.hpp advance): one pass per
-// sample, or the split schedule's light / eye passes.
-constexpr int kPhaseAll = 0, kPhaseLight = 1, kPhaseEye = 2;
 #ifndef BDPT_TRAV_WHILE_WHILE
 #define BDPT_TRAV_WHILE_WHILE 1  // megakernel traversal loop shape (0: one node or leaf per iteration)
 #endif

@@ -75,14 +75,9 @@ struct KParams {
     uint32_t nslots;
     unsigned long long* work;
     unsigned long long* counters;
-    // split schedule (kPhaseLight / kPhaseEye): this batch is samples
-    // [batch_base, batch_base + batch_n) of the shard; light vertices and parked
-    // samples are indexed by the position in the batch
-    float4* park;
-    uint64_t batch_base, batch_n;
 };
 
-template <bool FULL, bool COUNT, int PHASE>
+template <bool FULL, bool COUNT>
 __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(const KParams* __restrict__ kpp) {
     const KParams& kp = *kpp;
     __shared__ uint2 stack_mem[kLdsStack * kBlock];
@@ -91,13 +86,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     const Stack stk{stack_mem + threadIdx.x, kBlock, kLdsStack, kp.gstack, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
-    constexpr bool kSplit = PHASE != kPhaseAll;
-    // light-vertex / park slot: the lane (combined machine) or the sample's batch position (split)
-    uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
-    unsigned long long* const work = kp.work + (PHASE == kPhaseEye ? 1 : 0);
-    const uint64_t total = kSplit ? kp.batch_n : kp.fr.total_samples;
-    const uint64_t sample0 = kSplit ? kp.batch_base : 0;
-    const ParkStore park{kp.park};
+    const LightStore ls = light_store(kp.lv, kp.fr.rr_depth, blockIdx.x * kBlock + threadIdx.x);
+    unsigned long long* const work = kp.work;
+    const uint64_t total = kp.fr.total_samples;
     __shared__ LaneCold cold_mem[kBlock];
     Lane L(cold_mem[threadIdx.x]);
     L.state = ST_IDLE;
@@ -125,23 +116,6 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         uint64_t pa = (uint64_t)(ConstKParams)kpp;
         asm volatile("" : "+s"(pa));
         const KParams* P = (const KParams*)(ConstKParams)pa;
-        if constexpr (PHASE == kPhaseEye) {
-            // Resume parked samples: one atomic per wave for the idle lanes; a
-            // sample that ended in the light pass is skipped.
-            while (!exhausted) {
-                const uint64_t idle = __ballot(L.state == ST_IDLE);
-                if (!idle) break;
-                const int n = __popcll(idle);
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(work, static_cast<unsigned long long>(n));
-                base = __shfl(base, 0);
-                if (L.state == ST_IDLE) {
-                    const uint64_t j = base + __popcll(idle & ((1ull << lane) - 1ull));
-                    if (j < total && unpark_sample(park, static_cast<uint32_t>(j), L)) slot = static_cast<uint32_t>(j);
-                }
-                if (base + n >= total) exhausted = true;
-            }
-        } else {
 #if BDPT_SEED_CHUNK
         // Refill idle lanes from the wave's chunk of 64 consecutive samples. A
         // chunk is claimed with one atomic and the seeding recurrence of all its
@@ -167,15 +141,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 chunk_pos = 0;
                 global_done = base + 64 >= total;
                 int px;
-                chunk_x397 = mt_x397(sample_seed(sample0 + base + lane, P->fr, px));
+                chunk_x397 = mt_x397(sample_seed(base + lane, P->fr, px));
             }
             const int m = min(__popcll(idle), chunk_n - chunk_pos);
             const int rank = __popcll(idle & ((1ull << lane) - 1ull));
             const uint32_t x397 = __shfl(chunk_x397, (chunk_pos + rank) & 63);
-            if (L.state == ST_IDLE && rank < m) {
-                start_sample<true>(L, sample0 + chunk_base + chunk_pos + rank, P->fr, x397);
-                if (kSplit) slot = static_cast<uint32_t>(chunk_base + chunk_pos + rank);
-            }
+            if (L.state == ST_IDLE && rank < m) start_sample<true>(L, chunk_base + chunk_pos + rank, P->fr, x397);
             chunk_pos += m;
         }
 #else
@@ -189,16 +160,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 base = __shfl(base, leader);
                 if (L.state == ST_IDLE) {
                     const uint64_t s = base + __popcll(idle & ((1ull << lane) - 1ull));
-                    if (s < total) {
-                        start_sample(L, sample0 + s, P->fr);
-                        if (kSplit) slot = static_cast<uint32_t>(s);
-                    }
+                    if (s < total) start_sample(L, s, P->fr);
                 }
                 if (base + n >= total) exhausted = true;
             }
         }
 #endif
-        }
         if (__ballot(L.state != ST_IDLE) == 0) {
             if (exhausted) break;
             continue;
@@ -256,7 +223,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const uint64_t r0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
             const uint32_t act = resolve<COUNT>(L, res, rt, ru, rv, P->sc, P->fr, P->fb, cnt);
             if (COUNT && first_active_lane()) cnt.c[20] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - r0);
-            advance<COUNT, PHASE>(L, act, P->sc, P->fr, P->fb, light_store(P->lv, P->fr.rr_depth, slot), cnt, park, slot);
+            advance<COUNT>(L, act, P->sc, P->fr, P->fb, ls, cnt);
         }
         if (COUNT && first_active_lane()) {
             const uint64_t c2 = __builtin_amdgcn_s_memtime();
@@ -264,8 +231,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             cnt.c[13] += static_cast<uint32_t>(c2 - c1);
         }
 #else
-        static_assert(PHASE == kPhaseAll, "the split schedule needs the overlapped loop");
-        if (L.state != ST_IDLE) step<FULL, COUNT>(L, P->sc, P->fr, P->fb, light_store(P->lv, P->fr.rr_depth, slot), stk, cnt);
+        if (L.state != ST_IDLE) step<FULL, COUNT>(L, P->sc, P->fr, P->fb, ls, stk, cnt);
 #endif
     }
     if (COUNT) {
@@ -316,39 +282,20 @@ size_t frame_params_bytes() { return sizeof(dev::KParams); }
 
 // `dparams` is a device buffer of frame_params_bytes() owned by the caller; it
 // is filled on `stream` before the launch (stream order protects reuse).
-// phase: dev::kPhaseAll (one pass per sample), or the split schedule's
-// dev::kPhaseLight / kPhaseEye over samples [batch_base, batch_base + batch_n)
-// of the shard (light vertices and parked samples batch-indexed in lvbuf / park;
-// the eye pass takes its samples from work[1]).
 hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
                         uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
-                        hipStream_t stream, void* dparams, int phase, float4* park, uint64_t batch_base,
-                        uint64_t batch_n, bool write_params) {
+                        hipStream_t stream, void* dparams) {
     const bool full = (fr.flags & 2u) != 0, count = (fr.flags & 1u) != 0;
-    if (write_params) {
-        const dev::KParams host{sc, fr, fb, lvbuf, gstack, nslots, work, counters, park, batch_base, batch_n};
-        hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);
-        if (e != hipSuccess) return e;
-    }
+    const dev::KParams host{sc, fr, fb, lvbuf, gstack, nslots, work, counters};
+    hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
     const dev::KParams* kp = static_cast<const dev::KParams*>(dparams);
     const dim3 g(grid), b(dev::kBlock);
     const size_t lds = 4 * static_cast<size_t>(sc.lds_words);
-#define BDPT_LAUNCH(PH)                                                                                      \
-    do {                                                                                                     \
-        if (full && count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, true, PH>), g, b, lds, stream, kp); \
-        else if (full) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, false, PH>), g, b, lds, stream, kp);  \
-        else if (count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, true, PH>), g, b, lds, stream, kp); \
-        else hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, false, PH>), g, b, lds, stream, kp);           \
-    } while (0)
-#if BDPT_DEEP_RNG
-    (void)phase;
-    BDPT_LAUNCH(dev::kPhaseAll);
-#else
-    if (phase == dev::kPhaseLight) BDPT_LAUNCH(dev::kPhaseLight);
-    else if (phase == dev::kPhaseEye) BDPT_LAUNCH(dev::kPhaseEye);
-    else BDPT_LAUNCH(dev::kPhaseAll);
-#endif
-#undef BDPT_LAUNCH
+    if (full && count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, true>), g, b, lds, stream, kp);
+    else if (full) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, false>), g, b, lds, stream, kp);
+    else if (count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, true>), g, b, lds, stream, kp);
+    else hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, false>), g, b, lds, stream, kp);
     return hipGetLastError();
 }
 
@@ -368,8 +315,7 @@ hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float
 // Resident 256-lane blocks per CU for the frame kernel (VGPR and LDS limited).
 int frame_kernel_blocks_per_cu(size_t dyn_lds) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::bdpt_frame_kernel<false, false, dev::kPhaseAll>,
-                                                     dev::kBlock, dyn_lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::bdpt_frame_kernel<false, false>, dev::kBlock, dyn_lds) !=
             hipSuccess ||
         n <= 0)
         n = BDPT_WAVES_PER_EU;

@@ -71,11 +71,7 @@ __device__ __forceinline__ void store_vertex(const LightStore& ls, int v, const 
 }
 
 __device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
-#if BDPT_PROBE_LV_CACHED  // timing probe only (wrong results): every lane reads slot 0's records
-    const float4* q = ls.base + static_cast<size_t>(v) * 4;
-#else
     const float4* q = ls.at(v);
-#endif
     const float4 a = lv_ld(q), b = lv_ld(q + 1), c = lv_ld(q + 2), d = lv_ld(q + 3);
     Vertex x;
     x.p = xyz(a), x.vcm = a.w;
@@ -295,69 +291,12 @@ __device__ __forceinline__ void tally_action(Counts& cnt, bool on) {
     }
 }
 
-// Schedules of the state machine. kPhaseAll: a lane runs its sample from the
-// camera ray to the end (the megakernel). The split schedule runs a batch of
-// samples in two passes over the same machine: kPhaseLight runs render()'s
-// primary ray and lightSubpathWalk (bdpt.h:219-229, :158-217) and parks the
-// sample at the start of eyeSubpathWalk; kPhaseEye resumes every parked sample
-// there and runs the eye subpath with its connections (bdpt.h:46-155). Each
-// pass compiles only its own action bodies, so a shading step executes about
-// half the bodies of the combined machine with more lanes in each. The order
-// of the sample's random numbers and arithmetic is unchanged: the parked
-// record carries the generator state and everything the eye walk reads.
-// (kPhaseAll / kPhaseLight / kPhaseEye: bdpt_device.hpp)
-
-// Parked sample (4 float4, batch-indexed): (rng a0 a1 b n) (cam_d, pixel)
-// (primary t u v, primary triangle) (light vertices, steps - 1, live, 0).
-struct ParkStore {
-    float4* __restrict__ base;
-};
-// steps_adj: the eye pass re-enters through one ST_DEFER resolve, which counts a
-// query step; a sample the combined machine would also have routed through
-// ST_DEFER (its light walk ended at a BSDF sample or the depth cap) keeps its
-// count (0), one that goes straight to A_START_EYE gives that step back (-1).
-__device__ __forceinline__ void park_sample(const ParkStore& ps, uint32_t j, const Lane& L, bool live, int steps_adj) {
-    float4* q = ps.base + 4 * static_cast<size_t>(j);
-    if (live) {
-        gst4(q, make_float4(__uint_as_float(L.rng.a0), __uint_as_float(L.rng.a1), __uint_as_float(L.rng.b),
-                            __uint_as_float(L.rng.n)));
-        gst4(q + 1, make_float4(L.c.cam_d.x, L.c.cam_d.y, L.c.cam_d.z, __int_as_float(L.c.pixel)));
-        gst4(q + 2, make_float4(L.c.Li.x, L.c.Li.y, L.c.Li.z, __int_as_float(L.c.prim_tri)));
-    }
-    gst4(q + 3, make_float4(__int_as_float(L.c.nl), __int_as_float(L.c.steps + steps_adj),
-                            __int_as_float(live ? 1 : 0), 0.f));
-}
-// Resumes parked sample j on this lane (ST_DEFER: its next shading step runs
-// A_START_EYE); false when the sample ended in the light pass.
-__device__ __forceinline__ bool unpark_sample(const ParkStore& ps, uint32_t j, Lane& L) {
-    const float4* q = ps.base + 4 * static_cast<size_t>(j);
-    const float4 d = gld4(q + 3);
-    if (__float_as_int(d.z) == 0) return false;
-    const float4 a = gld4(q), b = gld4(q + 1), c = gld4(q + 2);
-    L.rng = LazyMT{__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z), __float_as_uint(a.w)};
-    L.c.cam_d = xyz(b), L.c.pixel = __float_as_int(b.w);
-    L.c.Li = xyz(c), L.c.prim_tri = __float_as_int(c.w);
-    L.c.nl = __float_as_int(d.x), L.c.steps = __float_as_int(d.y);
-    L.state = ST_DEFER;
-    return true;
-}
-
-template <bool COUNT, int PHASE = kPhaseAll>
+template <bool COUNT>
 __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
-                        const LightStore& ls, Counts& cnt, const ParkStore& park = ParkStore{nullptr},
-                        uint32_t park_slot = 0) {
+                        const LightStore& ls, Counts& cnt) {
     const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
     const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
-    constexpr bool kLight = PHASE != kPhaseEye, kEye = PHASE != kPhaseLight;
-    if constexpr (PHASE == kPhaseLight) {
-        // the light pass ends a sample where eyeSubpathWalk (or the sample) would start
-        if (act == A_START_EYE || act == A_FINISH) {
-            park_sample(park, park_slot, L, act == A_START_EYE, -1);
-            L.state = ST_IDLE;
-            act = A_DONE;
-        }
-    }
-    BDPT_ACTION(21, kEye && act == A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
+    BDPT_ACTION(21, act == A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
         const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
         if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
             const int mat = __float_as_int(gld4(sc.shade + 5 * static_cast<size_t>(L.c.prim_tri)).w);
@@ -385,7 +324,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             act = A_EYE_VERTEX;
         }
     } BDPT_END;
-    BDPT_ACTION(22, kEye && act == A_EYE_VERTEX) {  // bdpt.h:73-136
+    BDPT_ACTION(22, act == A_EYE_VERTEX) {  // bdpt.h:73-136
         const float dist2 = L.h.dist * L.h.dist;
         const float absCosIn = fabsf(L.h.wo.z);
         L.c.vcm *= div_cr(dist2, absCosIn);
@@ -428,10 +367,10 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
     int e_id = 0;
     float e_pdf = 0.f, e_pos_pdf = 0.f;
     f3 e_n = mk(0.f, 0.f, 0.f), e_p = e_n;
-    BDPT_ACTION(23, (kLight && act == A_START_LIGHT) || (kEye && act == A_NEE)) {
+    BDPT_ACTION(23, act == A_START_LIGHT || act == A_NEE) {
         e_id = sample_emitter(sc, L.rng, e_pdf, e_n, e_p, e_pos_pdf);
     } BDPT_END;
-    BDPT_ACTION(24, kLight && act == A_START_LIGHT) {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
+    BDPT_ACTION(24, act == A_START_LIGHT) {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
         const EmitterRecord& e = emitter_of(sc, e_id);
         float areaPdf = e_pos_pdf;
         const f3 edir = uniform_hemisphere(next2(L.rng));
@@ -453,7 +392,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             act = A_LIGHT_NEXT;
         }
     } BDPT_END;
-    BDPT_ACTION(25, kEye && act == A_NEE) {  // connectToLight (bdpt.h:374-430): everything but the visibility test
+    BDPT_ACTION(25, act == A_NEE) {  // connectToLight (bdpt.h:374-430): everything but the visibility test
         act = A_CONN;
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         const EmitterRecord& e = emitter_of(sc, e_id);
@@ -477,7 +416,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         L.state = ST_NEE;
         act = A_ISSUED;
     } BDPT_END;
-    BDPT_ACTION(26, kLight && act == A_LIGHT_VERTEX) {  // bdpt.h:193-209
+    BDPT_ACTION(26, act == A_LIGHT_VERTEX) {  // bdpt.h:193-209
         const float dist2 = L.h.dist * L.h.dist;
         const float absCosIn = fabsf(L.h.wo.z);
         L.c.vcm *= div_cr(dist2, absCosIn);
@@ -516,7 +455,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         L.state = ST_SPLAT;
         act = A_ISSUED;
     } BDPT_END;
-    BDPT_ACTION(27, kEye && act == A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
+    BDPT_ACTION(27, act == A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
         act = A_EYE_CONTINUE;
         if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
         const BsdfRecord& be = bsdf_of(sc, L.h.mat);
@@ -553,8 +492,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         }
     } BDPT_END;
     // ContinuePathRandomWalk of either subpath (light: bdpt.h:211-215, eye: bdpt.h:152).
-    BDPT_ACTION(28, (kLight && act == A_LIGHT_CONTINUE) || (kEye && act == A_EYE_CONTINUE)) {
-        const bool light = kLight && (!kEye || act == A_LIGHT_CONTINUE);
+    BDPT_ACTION(28, act == A_LIGHT_CONTINUE || act == A_EYE_CONTINUE) {
+        const bool light = act == A_LIGHT_CONTINUE;
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         const bool delta = is_delta(b);
         if (light && !delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, 1.f);  // the pre-walk state
@@ -572,7 +511,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             act = A_ISSUED;
         }
     } BDPT_END;
-    BDPT_ACTION(29, kLight && act == A_LIGHT_NEXT) {  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
+    BDPT_ACTION(29, act == A_LIGHT_NEXT) {  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
         if (!(L.c.depth < fr.rr_depth)) {
             (void)next1(L.rng);
             L.state = ST_DEFER;  // the eye subpath starts next step
@@ -581,7 +520,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         }
         act = A_ISSUED;
     } BDPT_END;
-    BDPT_ACTION(30, kEye && act == A_EYE_NEXT) {  // bdpt.h:68
+    BDPT_ACTION(30, act == A_EYE_NEXT) {  // bdpt.h:68
         if (!(L.c.depth < fr.rr_depth)) {
             (void)next1(L.rng);
             act = A_FINISH;
@@ -590,16 +529,10 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             act = A_ISSUED;
         }
     } BDPT_END;
-    BDPT_ACTION(31, kEye && act == A_FINISH) {
+    BDPT_ACTION(31, act == A_FINISH) {
         finish<COUNT>(L, fr, fb, cnt);
         act = A_DONE;
     } BDPT_END;
-    if constexpr (PHASE == kPhaseLight) {
-        if (L.state == ST_DEFER) {  // the light walk ended: park at once instead of one more shading step
-            park_sample(park, park_slot, L, true, 0);
-            L.state = ST_IDLE;
-        }
-    }
 }
 #undef BDPT_ACTION
 #undef BDPT_END

@@ -75,9 +75,6 @@ extern "C" {
 #define BDPT_FLAG_COUNT 1u            /* counting pass: fill bdpt_stats.counters (slower) */
 #define BDPT_FLAG_FULL_TRAVERSAL 2u   /* visit every box the reference visits (no t-culling) */
 #define BDPT_FLAG_WAVEFRONT 4u        /* wavefront passes (shade / trace kernels) instead of the megakernel */
-#define BDPT_FLAG_COMBINED 8u         /* megakernel running each sample's light and eye subpaths in one pass
-                                         (default for rr_depth <= 28: the split light / eye passes over
-                                         batches of samples; rr_depth > 28 always runs combined) */
 
 typedef struct bdpt_scene bdpt_scene; /* host-side ingested scene */
 typedef struct bdpt_ctx bdpt_ctx;     /* device context (one HIP device) */

@@ -58,11 +58,7 @@ def report(fb, ref):
     return e.max(), exact, whole
 
 
-SCHEDULES = [0, bdpt_amd.FLAG_COMBINED, bdpt_amd.FLAG_WAVEFRONT]
-SCHEDULE_IDS = ["split", "combined", "wavefront"]
-
-
-@pytest.mark.parametrize("sched", SCHEDULES, ids=SCHEDULE_IDS)
+@pytest.mark.parametrize("sched", [0, bdpt_amd.FLAG_WAVEFRONT], ids=["megakernel", "wavefront"])
 @pytest.mark.parametrize("name", FB_CASES)
 def test_gpu_matches_reference_golden(name, sched, golden_manifest):
     m = golden_manifest["framebuffers"][name]
@@ -75,7 +71,7 @@ def test_gpu_matches_reference_golden(name, sched, golden_manifest):
     assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact floats {exact:.4f}, image {whole:.3g})"
 
 
-@pytest.mark.parametrize("sched", SCHEDULES, ids=SCHEDULE_IDS)
+@pytest.mark.parametrize("sched", [0, bdpt_amd.FLAG_WAVEFRONT])
 def test_gpu_full_traversal_equals_culled_traversal(sched):
     """The reference's own binary tree walked without culling (FULL) and the
     4-wide hierarchy with distance culling give the same closest hits."""
@@ -84,29 +80,6 @@ def test_gpu_full_traversal_equals_culled_traversal(sched):
     b = integrator("caustic", 64, 64, 16, 8)
     fb = b.render_frame(flags=bdpt_amd.FLAG_FULL_TRAVERSAL | sched).copy()
     assert rel_l2(fa, fb).max() <= TOL
-
-
-@pytest.mark.parametrize("batch", [1, 777, 4096])
-def test_gpu_split_schedule_batches(batch, golden_manifest, monkeypatch):
-    """The split light / eye passes over batches of samples (BDPT_SPLIT_BATCH):
-    the smallest batch (64 samples, one wave's refill chunk), a ragged last batch,
-    and whole rows; every batch parks its samples and light vertices at batch
-    positions."""
-    name = "G3_hardlight_64x64_spp16"
-    m = golden_manifest["framebuffers"][name]
-    monkeypatch.setenv("BDPT_SPLIT_BATCH", str(batch))
-    if batch == 1:
-        it = integrator("hardlight", 16, 12, 2, m["rr_depth"])
-        fb = it.render_frame().reshape(-1)
-        assert it.stats()["launches"] == 2 * (16 * 12 * 2 // 64)
-        ref, _ = O.Scene(variants.obj_path("hardlight")).render(
-            O.make_params(variants.SCENES["hardlight"]["camera"], 16, 12, 2, m["rr_depth"]))
-    else:
-        it = integrator(m["scene"], m["width"], m["height"], m["spp"], m["rr_depth"])
-        fb = it.render_frame().reshape(-1)
-        assert it.stats()["launches"] == 2 * -(-m["samples"] // batch)
-        ref = load_golden(name)
-    assert report(fb, ref)[0] <= TOL
 
 
 @pytest.mark.parametrize("name,W,H,spp,rr", [
