@@ -37,9 +37,9 @@ __device__ __forceinline__ LightStore light_store(float* lv, int rr_depth, uint3
     return LightStore{reinterpret_cast<float4*>(lv), static_cast<uint32_t>(rr_depth > 1 ? rr_depth - 1 : 1), slot};
 }
 
-struct Vertex {  // PathVertex (bdpt.h:24-35)
-    f3 p, s, t, n, wo, tp;
-    float vcm, vc, rr;
+struct Vertex {  // PathVertex (bdpt.h:24-35); its Frame is rebuilt from n where used, rr is 1 (NO_RR)
+    f3 p, n, wo, tp;
+    float vcm, vc;
     int mat;
 };
 
@@ -76,9 +76,8 @@ __device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
     Vertex x;
     x.p = xyz(a), x.vcm = a.w;
     x.n = xyz(b), x.vc = b.w;
-    x.wo = xyz(c), x.rr = c.w;
+    x.wo = xyz(c);  // c.w: the vertex's rr, always 1 under NO_RR (bdpt.h:18): x * rr == x
     x.tp = xyz(d), x.mat = __float_as_int(d.w);
-    make_frame(x.n, x.s, x.t);  // Frame(n) is a pure function of n: identical s, t
     return x;
 }
 
@@ -465,7 +464,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             f3 dir = L.h.p - V.p;
             const float invD2 = rcp_cr(dot(dir, dir));
             dir = dir * sqrt_cr(invD2);
-            const f3 wiL = to_local(V.s, V.t, V.n, dir);
+            const f3 wiL = local_at(V.n, dir);  // Frame(n) is a pure function of n
             const f3 wiE = local_at(L.h.n, -dir);
             const float cosL = wiL.z, cosE = wiE.z;
             if (cosL <= 0.f || cosE <= 0.f) {
@@ -475,8 +474,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             const BsdfRecord& bl = bsdf_of(sc, V.mat);
             f3 Li = bsdf_eval(bl, wiL, V.wo) * bsdf_eval(be, wiE, L.h.wo);
             Li = Li * ((V.tp * L.c.tp) * invD2);
-            const float eyePathRev_w = bsdf_pdf(bl, wiL, V.wo) * V.rr;
-            const float lightPrevRev = bsdf_pdf(bl, V.wo, wiL) * V.rr;
+            const float eyePathRev_w = bsdf_pdf(bl, wiL, V.wo) * 1.f;  // * vertex rr (1)
+            const float lightPrevRev = bsdf_pdf(bl, V.wo, wiL) * 1.f;
             const float lightPathRev_w = bsdf_pdf(be, wiE, L.h.wo) * 1.f;
             const float eyePrevRev = bsdf_pdf(be, L.h.wo, wiE) * 1.f;
             const float lightPathRev_a = lightPathRev_w * cosL * invD2;
