@@ -312,8 +312,10 @@ def main() -> None:
             for k in ("active_lane_frac", "valu_issue_frac", "wait_frac", "valu_insts_per_sample"):
                 roof[k] = deep.get(k)
             roof["issue_source"] = deep.get("source")
+        default_workload = (args.scene, W, H, spp) == ("caustic", 512, 512, 256)
         out = {
-            "metric": METRIC,
+            "metric": METRIC if default_workload else f"Msamples/sec (whole node), {SCENE_LABEL.get(args.scene, args.scene)} "
+                                                      f"{W}x{H} at {spp} spp",
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
