@@ -195,12 +195,20 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N > 1 path on a one-GPU box (never the driver's runs):
+    # BDPT_BENCH_REHEARSAL=1 puts every rank on device 0 and reduces over gloo
+    # (RCCL cannot form a communicator with one device twice).
+    rehearsal = os.environ.get("BDPT_BENCH_REHEARSAL") == "1"
+    gpu = 0 if rehearsal else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", gpu if world > 1 else 0)
 
     sc = variants.SCENES[args.scene]
     rr = args.rr_depth or sc["rr_depth"]
@@ -208,14 +216,14 @@ def main() -> None:
     cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**sc["camera"]), width=W, height=H, spp=spp, rr_depth=rr)
     if args.integrator == "path":
         integ = bdpt_amd.PathTracerIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
-                                              bdpt_amd.PathSettings(), device=local if world > 1 else 0)
+                                              bdpt_amd.PathSettings(), device=gpu if world > 1 else 0)
     elif args.integrator == "direct":
         integ = bdpt_amd.DirectIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
                                           bdpt_amd.DirectSettings(sampling_strategy="mis"),
-                                          device=local if world > 1 else 0)
+                                          device=gpu if world > 1 else 0)
     else:
         integ = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
-                                        device=local if world > 1 else 0)
+                                        device=gpu if world > 1 else 0)
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -249,7 +257,7 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     samples_total = W * H * spp  # all ranks together, per step
@@ -274,7 +282,7 @@ def main() -> None:
     elif rank == 0:
         # algorithmic bytes per sample from a counting pass (untimed, same seeds, smaller spp)
         cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=min(spp, 16), rr_depth=rr)
-        cnt = bdpt_amd.BDPTIntegrator(integ.scene, cnt_cfg, device=local if world > 1 else 0)
+        cnt = bdpt_amd.BDPTIntegrator(integ.scene, cnt_cfg, device=gpu if world > 1 else 0)
         cbuf = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
         cnt.render_device(cbuf.data_ptr(), stream, flags=bdpt_amd.FLAG_COUNT | sched_flags)
         cst = cnt.stats()

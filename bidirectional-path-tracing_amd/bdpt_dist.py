@@ -29,4 +29,10 @@ def reduce_framebuffer(fb, dst: int = 0) -> None:
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.reduce(fb, dst=dst, op=dist.ReduceOp.SUM)
+        if dist.get_backend() == "gloo" and fb.is_cuda:  # gloo reduces host tensors
+            host = fb.cpu()
+            dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM)
+            if dist.get_rank() == dst:
+                fb.copy_(host)
+        else:
+            dist.reduce(fb, dst=dst, op=dist.ReduceOp.SUM)

@@ -151,3 +151,24 @@ def test_gpu_cli_devices_flag(golden_manifest, tmp_path):
     img = decode_exr((tmp_path / "scene.exr").read_bytes()).astype(np.float32)
     ref = load_golden(name).reshape(m["height"], m["width"], 3).astype(np.float16).astype(np.float32)
     assert np.allclose(img, ref, rtol=2 ** -10, atol=0)
+
+
+def test_gpu_bench_two_rank_rehearsal(tmp_path):
+    """bench.py's N > 1 path (torch.distributed.run, one rank per device, barrier +
+    max-over-ranks timing, row shards, the framebuffer reduce, rank 0's JSON line)
+    rehearsed on this one-GPU box: BDPT_BENCH_REHEARSAL=1 puts both ranks on GPU 0
+    and reduces over gloo instead of RCCL."""
+    import json
+    import sys
+
+    env = dict(os.environ, BDPT_BENCH_REHEARSAL="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--width", "64", "--height", "64", "--spp", "4",
+           "--no-cpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["samples_per_step"] == 64 * 64 * 4
