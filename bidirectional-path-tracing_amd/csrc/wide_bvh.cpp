@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 
@@ -49,9 +50,9 @@ class Builder {
     int max_depth = 0;
     bool median_only = false;
     // Leaves of up to max_leaf items, closed by the SAH (leaf cost n * area vs
-    // kNodeCost * area + the best split); max_leaf 1 = one item per leaf.
+    // node_cost * area + the best split); max_leaf 1 = one item per leaf.
     int max_leaf = 1;
-    static constexpr double kNodeCost = 1.0;
+    double node_cost = 1.0;
 
     int build(int b, int e, int depth) {
         max_depth = std::max(max_depth, depth);
@@ -67,7 +68,7 @@ class Builder {
         }
         double split_cost = 0.0;
         const int mid = split(b, e, &split_cost);
-        if (e - b <= max_leaf && box.area() * (e - b) <= kNodeCost * box.area() + split_cost) {
+        if (e - b <= max_leaf && box.area() * (e - b) <= node_cost * box.area() + split_cost) {
             nodes[id].leaf = b;
             nodes[id].count = e - b;
             return id;
@@ -295,13 +296,20 @@ bool build_wide_bvh_tris(const std::vector<FlatNode>& flat, const std::vector<fl
             it.box.hi[a] = std::nextafter(it.box.hi[a] + pad, __builtin_inff());
         }
     out.pad = pad;
+    // BDPT_TRI_LEAF_MAX / BDPT_SAH_NODE_COST override the builder (experiments)
+    int leaf_max = kTriLeafMax;
+    double node_cost = 1.0;
+    if (const char* e = std::getenv("BDPT_TRI_LEAF_MAX")) leaf_max = std::min(7, std::max(1, std::atoi(e)));
+    if (const char* e = std::getenv("BDPT_SAH_NODE_COST")) node_cost = std::max(0.0, std::atof(e));
     Builder B(items);
-    B.max_leaf = kTriLeafMax;
+    B.max_leaf = leaf_max;
+    B.node_cost = node_cost;
     B.build(0, static_cast<int>(n), 0);
     if (B.max_depth > kMaxBinaryDepth) {
         Builder M(items);
         M.median_only = true;
-        M.max_leaf = kTriLeafMax;
+        M.max_leaf = leaf_max;
+        M.node_cost = node_cost;
         M.build(0, static_cast<int>(n), 0);
         B.nodes.swap(M.nodes);
         B.max_depth = M.max_depth;
