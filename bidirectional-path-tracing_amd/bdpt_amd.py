@@ -155,6 +155,7 @@ def lib():
         L.bdpt_scene_free.argtypes = [vp]
         L.bdpt_scene_get_info.argtypes = [vp, ctypes.POINTER(_SceneInfo)]
         L.bdpt_scene_export.argtypes = [vp, vp, vp, vp, vp]
+        L.bdpt_scene_export_traversal.argtypes = [vp, vp, vp, vp, vp]
         L.bdpt_camera_constants.argtypes = [ctypes.POINTER(_Camera), i32, i32, f32p]
         L.bdpt_device_count.argtypes = [ctypes.POINTER(i32)]
         L.bdpt_ctx_create.argtypes = [vp, i32, ctypes.POINTER(vp)]
@@ -423,6 +424,18 @@ class Scene:
         nf, nu = np.zeros((m, 6), np.float32), np.zeros((m, 3), np.uint32)
         _check(lib().bdpt_scene_export(self._h, tf.ctypes.data, ti.ctypes.data, nf.ctypes.data, nu.ctypes.data))
         return tf, ti, nf, nu
+
+    def export_traversal(self):
+        """(wnodes[k,8,4], wtri[n,3,4], lbox[l,2,4], root_link): the traversal tree
+        (wide_bvh.hpp); the link / index / leaf-id words are uint32 bit patterns."""
+        inf = self.info()
+        wn = np.zeros((inf["wide_nodes"], 8, 4), np.float32)
+        wt = np.zeros((inf["triangles"], 3, 4), np.float32)
+        lb = np.zeros((inf["bvh_leaves"], 2, 4), np.float32)
+        root = ctypes.c_uint32()
+        _check(lib().bdpt_scene_export_traversal(self._h, wn.ctypes.data, wt.ctypes.data, lb.ctypes.data,
+                                                 ctypes.byref(root)))
+        return wn, wt, lb, int(root.value)
 
 
 def camera_constants(cam: Camera, width: int, height: int) -> np.ndarray:

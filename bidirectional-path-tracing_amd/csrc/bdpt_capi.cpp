@@ -258,6 +258,16 @@ int bdpt_scene_export(const bdpt_scene* s, float* tri_f32, int32_t* tri_i32, flo
     return BDPT_OK;
 }
 
+int bdpt_scene_export_traversal(const bdpt_scene* s, float* wnodes, float* wtri, float* lbox, uint32_t* root_link) {
+    if (!s) return fail(BDPT_ERR_INVALID, "null scene");
+    const DeviceLayout& L = s->layout;
+    if (wnodes) std::memcpy(wnodes, L.wnodes.data(), L.wnodes.size() * sizeof(float4_t));
+    if (wtri) std::memcpy(wtri, L.wtri.data(), L.wtri.size() * sizeof(float4_t));
+    if (lbox) std::memcpy(lbox, L.lbox.data(), L.lbox.size() * sizeof(float4_t));
+    if (root_link) *root_link = L.wroot_link;
+    return BDPT_OK;
+}
+
 int bdpt_camera_constants(const bdpt_camera* cam, int32_t width, int32_t height, float out[72]) {
     if (!cam || !out || width <= 0 || height <= 0) return fail(BDPT_ERR_INVALID, "bad camera arguments");
     CameraConstants c;

@@ -140,6 +140,11 @@ int bdpt_scene_get_info(const bdpt_scene* scene, bdpt_scene_info* out);
  * leaf order, tri_i32[ntri][3] = shapeID primID matID, node_f32[nnodes][6] =
  * bbox min/max, node_u32[nnodes][3] = start nPrims rightOffset (flat preorder). */
 int bdpt_scene_export(const bdpt_scene* scene, float* tri_f32, int32_t* tri_i32, float* node_f32, uint32_t* node_u32);
+/* Traversal-tree export (tests; wide_bvh.hpp): wnodes[wide_nodes][32] (8 float4:
+ * child lo.x hi.x lo.y hi.y lo.z hi.z link-bits unused), wtri[triangles][12]
+ * (v0|ref index bits, e1|ref leaf id bits, e2|0), lbox[bvh_leaves][8] (lo|0 hi|0),
+ * root_link. Any pointer may be NULL. */
+int bdpt_scene_export_traversal(const bdpt_scene* scene, float* wnodes, float* wtri, float* lbox, uint32_t* root_link);
 /* Camera constants: worldToCamera, cameraToWorld, cameraToClip, NDCToScreen
  * (column-major) then invWidth, invHeight, tan(fov/2), aspect, forward.xyz,
  * virtual near-plane distance — 72 floats. */
