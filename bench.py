@@ -183,8 +183,6 @@ def main() -> None:
                     help="bdpt = the hot path (BASELINE metric); path = the reference's PathTracerIntegrator "
                          "(path.h, cbox_bdpt_path.toml settings), direct = its DirectIntegrator (direct.h, MIS, "
                          "1 emitter + 1 BSDF sample) on the same substrate, for comparison")
-    ap.add_argument("--schedule", choices=["megakernel", "wavefront"], default="megakernel",
-                    help="render schedule (BDPT_FLAG_WAVEFRONT for the shade/trace passes)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the in-run parity check of the GPU row shard against the CPU reference frame")
     ap.add_argument("--profiles", default=os.path.join(REPO, "profiles"),
@@ -228,19 +226,16 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     kernel_ms = []
-    sched_flags = bdpt_amd.FLAG_WAVEFRONT if args.schedule == "wavefront" else 0
 
     row_offset, row_stride = bdpt_dist.row_shard(rank, world)
 
     def step():
         fb.zero_()
-        integ.render_device(fb.data_ptr(), stream, row_offset=row_offset, row_stride=row_stride, flags=sched_flags)
+        integ.render_device(fb.data_ptr(), stream, row_offset=row_offset, row_stride=row_stride)
         st = integ.stats()  # waits for the render kernel's end event
         kernel_ms.append(st["kernel_ms"])
-        if args.integrator == "path" and st["counters"]["shadow_rays"]:
-            # counters[1] of bdpt_render_path: samples that outgrew the 512-level
-            # recursion stack, whose result is then not the reference's
-            raise RuntimeError(f"{st['counters']['shadow_rays']} path samples outgrew the level stack")
+        if args.integrator == "path":
+            integ.check_levels()  # a sample past the 512-level stack would not be the reference's
         bdpt_dist.reduce_framebuffer(fb, dst=0)
 
     for _ in range(args.warmup):
@@ -284,7 +279,7 @@ def main() -> None:
         cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=min(spp, 16), rr_depth=rr)
         cnt = bdpt_amd.BDPTIntegrator(integ.scene, cnt_cfg, device=gpu if world > 1 else 0)
         cbuf = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
-        cnt.render_device(cbuf.data_ptr(), stream, flags=bdpt_amd.FLAG_COUNT | sched_flags)
+        cnt.render_device(cbuf.data_ptr(), stream, flags=bdpt_amd.FLAG_COUNT)
         cst = cnt.stats()
         cts = cst["counters"]
         bps = algorithmic_bytes_per_sample(cts, cst["samples"], SURVEY_BYTES)
@@ -300,9 +295,8 @@ def main() -> None:
         traffic = pm["hbm_bytes_per_launch"] * local_samples / pm["samples_per_launch"] if pm else None
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
-                "kernel": "bdpt_frame_kernel" if args.schedule == "megakernel"
-                else "bdpt_shade_kernel + bdpt_trace_kernel",
-                "kernel_build": build, "schedule": args.schedule, "kernel_ms": round(avg_kernel_ms, 3),
+                "kernel": "bdpt_frame_kernel",
+                "kernel_build": build, "schedule": "megakernel", "kernel_ms": round(avg_kernel_ms, 3),
                 "samples_per_launch": local_samples,
                 "byte_model": "SURVEY.md 8(d): 64 B/node visit, 36 B/triangle test, 40 B/closest hit, "
                               "64 B/light vertex written or read, 12 B/framebuffer add",
@@ -350,8 +344,7 @@ def main() -> None:
 
                 # the same row shard on the GPU, same seeds: framebuffer parity in this run
                 pbuf = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
-                integ.render_device(pbuf.data_ptr(), stream, row_offset=0, row_stride=cb["row_stride"],
-                                    flags=sched_flags)
+                integ.render_device(pbuf.data_ptr(), stream, row_offset=0, row_stride=cb["row_stride"])
                 torch.cuda.synchronize(dev)
                 ref = np.fromfile(ref_fb, np.float32)
                 os.unlink(ref_fb)

@@ -33,7 +33,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BDPT_AMD_LIB") or os.path.join(HERE, "lib", "libbdpt_amd.so")
 
 STRATEGY_BDPT, STRATEGY_LIGHT_TRACING, STRATEGY_PATH_TRACING = 0, 1, 2
-FLAG_COUNT, FLAG_FULL_TRAVERSAL, FLAG_WAVEFRONT = 1, 2, 4
+FLAG_COUNT, FLAG_FULL_TRAVERSAL = 1, 2
 REFERENCE_SEED = 260450963  # renderer.cpp:155
 COUNTER_NAMES = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
                  "light_vert_reads", "splats", "rng_draws", "trav_lane_iters", "trav_wave_iters",
@@ -599,9 +599,19 @@ class PathTracerIntegrator(BDPTIntegrator):
 
     def render_device(self, fb_ptr: int, stream_ptr: int = 0, row_offset: int = 0, row_stride: int = 1,
                       flags: int = 0) -> None:
+        """Asynchronous; call check_levels() after the stream is synchronised: a
+        sample that outgrew the 512-level recursion stack makes the frame differ
+        from the reference's (render_frame checks this itself)."""
         p, pp = self.params(row_offset, row_stride, flags), self.path.c()
         _check(lib().bdpt_render_path(self._h, ctypes.byref(p), ctypes.byref(pp), ctypes.c_void_p(fb_ptr),
                                       ctypes.c_void_p(stream_ptr)))
+
+    def check_levels(self) -> None:
+        """Raises BdptError if a sample of the last render_device call outgrew the
+        level stack (bdpt_get_stats counters[1] of bdpt_render_path)."""
+        n = self.stats()["counters"]["shadow_rays"]
+        if n:
+            raise BdptError(f"{n} path samples outgrew the 512-level recursion stack")
 
 
 class DirectIntegrator(BDPTIntegrator):

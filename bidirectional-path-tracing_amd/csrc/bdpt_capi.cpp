@@ -1,7 +1,7 @@
 // C-ABI implementation (include/bdpt_amd.h): scene ingest, device context,
 // frame and single-sample renders. Host code only; kernels live in
-// bdpt_wavefront.hip (default schedule) and bdpt_kernels.hip (megakernel,
-// single-sample kernel). No CPU fallback exists: every render runs the HIP kernels.
+// bdpt_kernels.hip (the BDPT megakernel), sample_state.hip (single-sample
+// kernels), pt_kernels.hip (path / direct) and kat_kernels.hip (per-function). No CPU fallback exists: every render runs the HIP kernels.
 #include "../../include/bdpt_amd.h"
 
 #include <hip/hip_runtime.h>
@@ -39,18 +39,6 @@ hipError_t launch_intersect_kat(const dev::DevScene& sc, int64_t n, int occlusio
                                 uint32_t nslots, float* out, hipStream_t st);
 hipError_t launch_splat_kat(const dev::DevFrame& fr, int64_t n, const float* p, int32_t* xy, hipStream_t st);
 int frame_kernel_lds_stack();
-size_t wf_params_bytes();
-int wf_lane_chunks();
-int wf_trace_block();
-int wf_trace_lds_stack();
-int wf_trace_blocks_per_cu();
-hipError_t wf_set_params(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lv, uint2* gstack,
-                         float4* lane, float4* ray, float4* res, unsigned long long* wctr, uint32_t* tctr,
-                         unsigned long long* counters, uint32_t* sstack, uint32_t nslots, uint32_t trace_lanes,
-                         int shade_lds, void* dparams, hipStream_t stream);
-hipError_t wf_launch_pass(const void* dparams, uint32_t flags, uint32_t nslots, int trace_grid, int shade_lds,
-                          uint32_t p_lds_words, int64_t pass, hipStream_t stream);
-int wf_parts();
 int frame_kernel_blocks_per_cu(size_t dyn_lds);
 // bdpt_kernels_deep.hip: the same megakernel for rrDepth > 28
 hipError_t launch_frame_deep(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf,
@@ -132,22 +120,6 @@ struct bdpt_ctx {
     size_t tmp_fb_floats = 0;
     float* sample_out = nullptr;
     void* dparams = nullptr;  // kernel parameter block (filled in stream order per launch)
-    // wavefront schedule (bdpt_wavefront.hip)
-    uint32_t wf_slots = 0;      // path slots allocated
-    float4* wf_lane = nullptr;  // chunks x slots
-    float4* wf_ray = nullptr;
-    float4* wf_res = nullptr;
-    unsigned long long* wf_wctr = nullptr;  // partitioned sample counters + done mask
-    uint32_t* wf_tctr = nullptr;            // per-parity slot cursors, done masks, issued flags
-    uint32_t* host_ctr = nullptr;           // pinned, 2 x 320 words (copies of wf_tctr)
-    void* wf_dparams = nullptr;
-    hipEvent_t chunk_ev[2] = {nullptr, nullptr};
-    int trace_grid = 0;
-    uint32_t trace_lanes = 0;
-    int shade_lds = 0;            // link-stack entries of the shade kernel held in LDS
-    int shade_depth = 0;          // entries the binary traversal can need
-    uint32_t* sstack = nullptr;   // overflow beyond shade_lds (scenes deeper than kShadeLdsMax)
-    uint32_t sstack_slots = 0;
     // path tracer (pt_kernels.hip): level stacks, generator rings, parameter block
     int pt_grid = 0;
     uint32_t pt_nslots = 0;
@@ -300,17 +272,11 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocs) (void)hipFree(p);
     for (void* p : {static_cast<void*>(c->work), static_cast<void*>(c->counters), static_cast<void*>(c->lv),
-                    static_cast<void*>(c->gstack), static_cast<void*>(c->wf_lane), static_cast<void*>(c->wf_ray),
-                    static_cast<void*>(c->wf_res), static_cast<void*>(c->wf_wctr), static_cast<void*>(c->wf_tctr),
-                    static_cast<void*>(c->sstack), c->wf_dparams,
-                    static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams,
+                    static_cast<void*>(c->gstack), static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams,
                     static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
                     static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state),
                     static_cast<void*>(c->splat_list)})
         if (p) (void)hipFree(p);
-    if (c->host_ctr) (void)hipHostFree(c->host_ctr);
-    for (hipEvent_t e : c->chunk_ev)
-        if (e) (void)hipEventDestroy(e);
     if (c->last_use) (void)hipEventDestroy(c->last_use);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -404,20 +370,9 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     // Traversal stack: worst case of either tree (binary: depth + 1 pending
     // right children; 4-wide: the host-computed bound), the part beyond the
     // kernel's LDS entries in HBM.
-    c->trace_grid = c->cus * wf_trace_blocks_per_cu();
-    c->trace_lanes = static_cast<uint32_t>(c->trace_grid * wf_trace_block());
     const int depth = std::max(s->host.max_depth + 2, L.wmax_stack + 1);
     const size_t spill_mega = static_cast<size_t>(std::max(0, depth - frame_kernel_lds_stack())) * c->nslots;
-    const size_t spill_wf = static_cast<size_t>(std::max(0, depth - wf_trace_lds_stack())) * c->trace_lanes;
-    HIP_TRY(hipMalloc(&c->gstack, sizeof(uint2) * std::max<size_t>(1, std::max(spill_mega, spill_wf))));
-    c->shade_depth = s->host.max_depth + 2;
-    c->shade_lds = std::min(c->shade_depth, 48);  // 48 KiB of LDS per 256-lane block at most
-    HIP_TRY(hipMalloc(&c->wf_wctr, (wf_parts() + 1) * sizeof(unsigned long long)));
-    HIP_TRY(hipMalloc(&c->wf_tctr, 320 * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&c->wf_dparams, wf_params_bytes()));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->host_ctr), 640 * sizeof(uint32_t), hipHostMallocDefault));
-    HIP_TRY(hipEventCreateWithFlags(&c->chunk_ev[0], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&c->chunk_ev[1], hipEventDisableTiming));
+    HIP_TRY(hipMalloc(&c->gstack, sizeof(uint2) * std::max<size_t>(1, spill_mega)));
     *out = c.release();
     return BDPT_OK;
 }
@@ -429,9 +384,8 @@ static int check_params(const bdpt_frame_params* p) {
         return fail(BDPT_ERR_INVALID, "image too large (W*H must fit int32, as in the reference)");
     if (p->rr_depth < 1 || p->rr_depth > kMaxRrDepth)
         return fail(BDPT_ERR_UNSUPPORTED, "rr_depth must be in [1, 1024]");
-    if (p->rr_depth > kLazyRrDepth && (p->flags & BDPT_FLAG_WAVEFRONT))
-        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 needs the megakernel schedule (the wavefront schedule "
-                                          "keeps the lazy MT19937 window only)");
+    if (p->flags & ~(BDPT_FLAG_COUNT | BDPT_FLAG_FULL_TRAVERSAL))
+        return fail(BDPT_ERR_UNSUPPORTED, "unknown flag (bit 2, the round-1 wavefront schedule, was removed)");
     if (p->strategy < 0 || p->strategy > 2) return fail(BDPT_ERR_INVALID, "unknown strategy");
     if (p->row_stride < 1 || p->row_offset < 0) return fail(BDPT_ERR_INVALID, "bad row shard");
     return BDPT_OK;
@@ -461,76 +415,6 @@ static int ensure_lv(bdpt_ctx* c, int rr_depth, uint32_t nslots) {
     return BDPT_OK;
 }
 
-// Path slots of the wavefront schedule: every in-flight camera sample owns one
-// (state, light vertices, pending query). 2^22 slots (~2.7 GB of HBM at rrDepth
-// 8) give each trace pass ~8 queries per lane; override with BDPT_WF_SLOTS.
-static uint32_t wavefront_slots(uint64_t total_samples) {
-    uint64_t cap = 1u << 22;
-    if (const char* e = std::getenv("BDPT_WF_SLOTS")) {
-        const long long v = std::atoll(e);
-        if (v >= 256 && v <= (1ll << 26)) cap = static_cast<uint64_t>(v);
-    }
-    const uint64_t n = std::min<uint64_t>(cap, (total_samples + 255) / 256 * 256);
-    return static_cast<uint32_t>(std::max<uint64_t>(n, 256));
-}
-
-static int ensure_wavefront(bdpt_ctx* c, uint32_t nslots) {
-    if (nslots <= c->wf_slots) return BDPT_OK;
-    for (void* q : {static_cast<void*>(c->wf_lane), static_cast<void*>(c->wf_ray), static_cast<void*>(c->wf_res)})
-        if (q) HIP_TRY(hipFree(q));
-    c->wf_lane = c->wf_ray = c->wf_res = nullptr;
-    HIP_TRY(hipMalloc(&c->wf_lane, sizeof(float4) * wf_lane_chunks() * static_cast<size_t>(nslots)));
-    HIP_TRY(hipMalloc(&c->wf_ray, sizeof(float4) * 2 * static_cast<size_t>(nslots)));
-    HIP_TRY(hipMalloc(&c->wf_res, sizeof(float4) * static_cast<size_t>(nslots)));
-    if (c->shade_depth > c->shade_lds) {
-        if (c->sstack) HIP_TRY(hipFree(c->sstack));
-        HIP_TRY(hipMalloc(&c->sstack,
-                          sizeof(uint32_t) * static_cast<size_t>(c->shade_depth - c->shade_lds) * nslots));
-    }
-    c->wf_slots = nslots;
-    return BDPT_OK;
-}
-
-// Wavefront schedule: passes of (shade, trace) in chunks of kChunk; the host
-// reads the issued-query flags of each chunk's last pass (pinned copy, one chunk
-// behind, so the GPU never idles) and stops once a pass issued no query —
-// then every sample of the shard is finished.
-static int render_wavefront(bdpt_ctx* c, const dev::DevFrame& fr, float* fb, hipStream_t st, int64_t& passes) {
-    constexpr int kChunk = 16;
-    constexpr int64_t kMaxPasses = 1ll << 24;
-    const uint32_t nslots = wavefront_slots(fr.total_samples);
-    int rc;
-    if ((rc = ensure_wavefront(c, nslots))) return rc;
-    if ((rc = ensure_lv(c, fr.rr_depth, nslots))) return rc;
-    // every slot idle (state 0) with no query (min_t NaN); all counters zero
-    HIP_TRY(hipMemsetAsync(c->wf_lane + nslots, 0, sizeof(float4) * nslots, st));
-    HIP_TRY(hipMemsetAsync(c->wf_ray, 0xff, sizeof(float4) * 2 * static_cast<size_t>(nslots), st));
-    HIP_TRY(hipMemsetAsync(c->wf_wctr, 0, (wf_parts() + 1) * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(c->wf_tctr, 0, 320 * sizeof(uint32_t), st));
-    HIP_TRY(wf_set_params(c->sc, fr, fb, c->lv, c->gstack, c->wf_lane, c->wf_ray, c->wf_res, c->wf_wctr, c->wf_tctr,
-                          c->counters, c->sstack, nslots, c->trace_lanes, c->shade_lds, c->wf_dparams, st));
-    int64_t k = 0;
-    for (int64_t chunk = 0;; chunk++) {
-        for (int j = 0; j < kChunk; j++, k++)
-            HIP_TRY(wf_launch_pass(c->wf_dparams, fr.flags, nslots, c->trace_grid, c->shade_lds, c->sc.lds_words, k,
-                                   st));
-        uint32_t* hc = c->host_ctr + 320 * (chunk & 1);
-        HIP_TRY(hipMemcpyAsync(hc, c->wf_tctr, 320 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipEventRecord(c->chunk_ev[chunk & 1], st));
-        if (chunk > 0) {
-            HIP_TRY(hipEventSynchronize(c->chunk_ev[(chunk - 1) & 1]));
-            const uint32_t* prev = c->host_ctr + 320 * ((chunk - 1) & 1);
-            const int last_parity = static_cast<int>((chunk * kChunk - 1) & 1);
-            uint32_t issued = 0;
-            for (int q = 0; q < wf_parts(); q++) issued |= prev[160 * last_parity + 96 + q];
-            if (!issued) break;  // the previous chunk ended with a pass that issued no query
-        }
-        if (k > kMaxPasses) return fail(BDPT_ERR_HIP, "wavefront schedule did not terminate");
-    }
-    passes = k;
-    return BDPT_OK;
-}
-
 int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_stream) {
     if (!c || !fb) return fail(BDPT_ERR_INVALID, "null argument");
     int rc = check_params(p);
@@ -538,10 +422,9 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const dev::DevFrame fr = make_frame(p);
-    const bool mega = (p->flags & BDPT_FLAG_WAVEFRONT) == 0;
-    if (mega && (rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
+    if ((rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
     dev::DevScene sc = c->sc;
-    if (mega && p->rr_depth > kLazyRrDepth) {  // draws past 226: the lanes' MT19937 rings
+    if (p->rr_depth > kLazyRrDepth) {  // draws past 226: the lanes' MT19937 rings
         if (!c->mt_ring) HIP_TRY(hipMalloc(&c->mt_ring, sizeof(uint32_t) * 624 * static_cast<size_t>(c->nslots)));
         sc.mt_ring = c->mt_ring;
         sc.mt_ring_stride = c->nslots;
@@ -552,22 +435,16 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     HIP_TRY(hipEventRecord(c->ev0, st));
     int64_t launches = 0;
     if (fr.total_samples > 0) {
-        if (mega) {
-            if (p->rr_depth > kLazyRrDepth) {  // never more resident blocks than the slots allocated
-                const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_deep(
-                                                               4 * static_cast<size_t>(c->sc.lds_words)));
-                HIP_TRY(launch_frame_deep(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
-                                          c->dparams));
-            } else {
-                HIP_TRY(launch_frame(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
-                                     c->dparams));
-            }
-            launches = 1;
+        if (p->rr_depth > kLazyRrDepth) {  // never more resident blocks than the slots allocated
+            const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_deep(
+                                                           4 * static_cast<size_t>(c->sc.lds_words)));
+            HIP_TRY(launch_frame_deep(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
+                                      c->dparams));
         } else {
-            int64_t passes = 0;
-            if ((rc = render_wavefront(c, fr, fb, st, passes))) return rc;
-            launches = 2 * passes;
+            HIP_TRY(launch_frame(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
+                                 c->dparams));
         }
+        launches = 1;
     }
     HIP_TRY(hipEventRecord(c->ev1, st));
     if ((rc = end_use(c, st))) return rc;

@@ -178,23 +178,23 @@ int bdpt_multi_create(const bdpt_scene* scene, int32_t ndevices, const int32_t* 
 int bdpt_multi_destroy(bdpt_multi* m) {
     if (!m) return BDPT_OK;
     for (size_t i = 0; i < m->devices.size(); i++) {
-        hipSetDevice(m->devices[i]);
-        if (m->stream[i]) hipStreamSynchronize(m->stream[i]);
+        (void)hipSetDevice(m->devices[i]);
+        if (m->stream[i]) (void)hipStreamSynchronize(m->stream[i]);
     }
     for (ncclComm_t c : m->comm)
         if (c) rccl().comm_destroy(c);
     for (size_t i = 0; i < m->devices.size(); i++) {
-        hipSetDevice(m->devices[i]);
-        if (m->fb[i]) hipFree(m->fb[i]);
-        if (m->stream[i]) hipStreamDestroy(m->stream[i]);
+        (void)hipSetDevice(m->devices[i]);
+        if (m->fb[i]) (void)hipFree(m->fb[i]);
+        if (m->stream[i]) (void)hipStreamDestroy(m->stream[i]);
         if (m->ctx[i]) bdpt_ctx_destroy(m->ctx[i]);
     }
     if (!m->devices.empty()) {
-        hipSetDevice(m->devices[0]);
-        if (m->stage) hipFree(m->stage);
-        if (m->t0) hipEventDestroy(m->t0);
-        if (m->t1) hipEventDestroy(m->t1);
-        if (m->t2) hipEventDestroy(m->t2);
+        (void)hipSetDevice(m->devices[0]);
+        if (m->stage) (void)hipFree(m->stage);
+        if (m->t0) (void)hipEventDestroy(m->t0);
+        if (m->t1) (void)hipEventDestroy(m->t1);
+        if (m->t2) (void)hipEventDestroy(m->t2);
     }
     delete m;
     return BDPT_OK;

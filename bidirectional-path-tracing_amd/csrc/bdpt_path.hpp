@@ -3,8 +3,8 @@
 // as a sequence of ray queries. A Lane holds the sample's state between
 // queries; resolve() applies a query's result and advance() runs the
 // integrator until the lane needs its next query (or finishes the sample).
-// The megakernel (bdpt_kernels.hip) keeps Lanes in registers; the wavefront
-// kernels (bdpt_wavefront.hip) keep them in HBM between passes.
+// The megakernel (bdpt_kernels.hip) and the single-sample kernels
+// (sample_state.hip) keep Lanes in registers (the cold part in LDS).
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -74,7 +74,7 @@ extern "C" {
 /* bdpt_frame_params.flags */
 #define BDPT_FLAG_COUNT 1u            /* counting pass: fill bdpt_stats.counters (slower) */
 #define BDPT_FLAG_FULL_TRAVERSAL 2u   /* visit every box the reference visits (no t-culling) */
-#define BDPT_FLAG_WAVEFRONT 4u        /* wavefront passes (shade / trace kernels) instead of the megakernel */
+/* (bit 2, the round-1 wavefront schedule, was removed: the megakernel beat it ~5x; now BDPT_ERR_UNSUPPORTED) */
 
 typedef struct bdpt_scene bdpt_scene; /* host-side ingested scene */
 typedef struct bdpt_ctx bdpt_ctx;     /* device context (one HIP device) */
@@ -99,8 +99,7 @@ typedef struct {
     bdpt_camera camera;
     int32_t width, height; /* [film] (the global image; shards still splat into it) */
     int32_t spp;           /* [renderer] spp */
-    int32_t rr_depth;      /* [renderer] rrDepth: hard path-depth cap (NO_RR=1, bdpt.h:18); 1..1024
-                              (1..28 with BDPT_FLAG_WAVEFRONT and bdpt_render_sample) */
+    int32_t rr_depth;      /* [renderer] rrDepth: hard path-depth cap (NO_RR=1, bdpt.h:18); 1..1024 */
     int32_t strategy;      /* BDPT_STRATEGY_* (reference default: BDPT) */
     uint32_t seed_base;    /* 260450963 = the reference's Sampler seed (renderer.cpp:155) */
     int32_t row_offset;    /* shard: render rows row_offset, row_offset+row_stride, ... */

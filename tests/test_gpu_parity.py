@@ -58,12 +58,11 @@ def report(fb, ref):
     return e.max(), exact, whole
 
 
-@pytest.mark.parametrize("sched", [0, bdpt_amd.FLAG_WAVEFRONT], ids=["megakernel", "wavefront"])
 @pytest.mark.parametrize("name", FB_CASES)
-def test_gpu_matches_reference_golden(name, sched, golden_manifest):
+def test_gpu_matches_reference_golden(name, golden_manifest):
     m = golden_manifest["framebuffers"][name]
     it = integrator(m["scene"], m["width"], m["height"], m["spp"], m["rr_depth"], STRATEGY[m.get("strategy", "bdpt")])
-    fb = it.render_frame(row_offset=0, row_stride=m["row_stride"], flags=sched).reshape(-1)
+    fb = it.render_frame(row_offset=0, row_stride=m["row_stride"]).reshape(-1)
     assert it.stats()["samples"] == m["samples"]
     ref = load_golden(name)
     worst, exact, whole = report(fb, ref)
@@ -71,14 +70,13 @@ def test_gpu_matches_reference_golden(name, sched, golden_manifest):
     assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact floats {exact:.4f}, image {whole:.3g})"
 
 
-@pytest.mark.parametrize("sched", [0, bdpt_amd.FLAG_WAVEFRONT])
-def test_gpu_full_traversal_equals_culled_traversal(sched):
+def test_gpu_full_traversal_equals_culled_traversal():
     """The reference's own binary tree walked without culling (FULL) and the
     4-wide hierarchy with distance culling give the same closest hits."""
     a = integrator("caustic", 64, 64, 16, 8)
-    fa = a.render_frame(flags=sched).copy()
+    fa = a.render_frame().copy()
     b = integrator("caustic", 64, 64, 16, 8)
-    fb = b.render_frame(flags=bdpt_amd.FLAG_FULL_TRAVERSAL | sched).copy()
+    fb = b.render_frame(flags=bdpt_amd.FLAG_FULL_TRAVERSAL).copy()
     assert rel_l2(fa, fb).max() <= TOL
 
 
@@ -121,10 +119,11 @@ def test_gpu_deep_rr_depth_continues_mt19937_from_ring(rr, W, H, spp, tmp_path):
 
 
 def test_gpu_rr_depth_limits():
-    """The wavefront schedule keeps the lazy window (rrDepth <= 28); past 1024 is refused."""
-    it = integrator("cbox_low", 8, 8, 1, 29)
-    with pytest.raises(bdpt_amd.BdptError, match="rr_depth"):
-        it.render_frame(flags=bdpt_amd.FLAG_WAVEFRONT)
+    """rrDepth past 1024 is refused, and so is an unknown flag (bit 2 was the
+    round-1 wavefront schedule)."""
+    it = integrator("cbox_low", 8, 8, 1, 8)
+    with pytest.raises(bdpt_amd.BdptError, match="flag"):
+        it.render_frame(flags=4)
     it = integrator("cbox_low", 8, 8, 1, 1025)
     with pytest.raises(bdpt_amd.BdptError, match="rr_depth"):
         it.render_frame()
@@ -159,7 +158,7 @@ def test_gpu_empty_shard_leaves_framebuffer_untouched():
     assert np.all(fb == 7.0)
 
 
-def driver_ray(p, name, pixel, k):
+def driver_ray(p, name, pixel, k, eye=None):
     """The camera ray and sampler the offline driver hands to render() for
     sample k of `pixel` (renderer.cpp:162-192: jitter draws first when spp > 1)."""
     W, spp = p.width, p.spp
@@ -179,7 +178,31 @@ def driver_ray(p, name, pixel, k):
     d = d * (f32(1) / np.sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]))
     sampler = bdpt_amd.Sampler.for_sample(pixel, spp, k)
     assert np.float32(sampler.next()) == u[0] and np.float32(sampler.next()) == u[1]  # the jitter draws
-    return bdpt_amd.Ray(tuple(variants.SCENES[name]["camera"]["eye"]), tuple(d), 1.0, 1000.0), sampler
+    eye = eye if eye is not None else variants.SCENES[name]["camera"]["eye"]
+    return bdpt_amd.Ray(tuple(eye), tuple(d), 1.0, 1000.0), sampler
+
+
+@pytest.mark.parametrize("rr", [40, 150])
+def test_gpu_single_sample_api_deep_rr_depth(rr, tmp_path):
+    """render(ray, sampler) past the lazy MT19937 window: in the closed box
+    every path runs to rrDepth (hundreds of draws per sample); the sample kernel
+    continues the caller's generator state in HBM, same Li, splats and final
+    generator state as the oracle."""
+    obj = variants.closed_box_obj(str(tmp_path))
+    cam = variants.CLOSED_CAMERA
+    W, H, spp = 8, 6, 2
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**cam), width=W, height=H, spp=spp, rr_depth=rr)
+    it = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(obj), cfg)
+    it.init()
+    p = O.make_params(cam, W, H, spp, rr)
+    sc = O.Scene(obj)
+    for pixel, k in [(0, 0), (27, 1), (47, 1)]:
+        it.rgb[:] = 0
+        Li_ref, splats_ref = sc.sample(p, pixel, k)
+        ray, sampler = driver_ray(p, None, pixel, k, eye=cam["eye"])
+        Li = it.render(ray, sampler)
+        assert np.allclose(Li, Li_ref, rtol=1e-6, atol=0), (pixel, Li, Li_ref)
+        assert rel_l2(it.rgb.reshape(-1), splats_ref).max() <= TOL
 
 
 @pytest.mark.parametrize("pixel,k", [(0, 0), (2080, 3), (1000, 15), (4095, 7), (2500, 9)])
@@ -227,24 +250,6 @@ def test_gpu_full_size_caustic_properties(golden_manifest):
     assert rel_l2(it2.render_frame(), fb).max() <= TOL
 
 
-@pytest.mark.parametrize("slots", ["256", "1000", "4096"])
-def test_gpu_wavefront_slot_pool_refills(slots, monkeypatch):
-    """Few path slots: every slot renders many samples in turn (partitioned
-    sample counters, slot chunks smaller than a wave) — same image as the oracle."""
-    monkeypatch.setenv("BDPT_WF_SLOTS", slots)
-    name, W, H, spp, rr = "caustic", 40, 24, 5, 8
-    fb = integrator(name, W, H, spp, rr).render_frame(flags=bdpt_amd.FLAG_WAVEFRONT).reshape(-1)
-    ref, _ = O.Scene(variants.obj_path(name)).render(O.make_params(variants.SCENES[name]["camera"], W, H, spp, rr))
-    worst, exact, _ = report(fb, ref)
-    assert worst <= TOL, f"slots={slots}: max per-pixel rel L2 {worst:.3g}"
-
-
-def test_gpu_megakernel_matches_wavefront():
-    a = integrator("hardlight_mirror", 48, 40, 6, 5).render_frame().copy()
-    b = integrator("hardlight_mirror", 48, 40, 6, 5).render_frame(flags=bdpt_amd.FLAG_WAVEFRONT).copy()
-    assert rel_l2(a, b).max() <= TOL
-
-
 def test_gpu_cli_renders_toml_to_reference_exr(tmp_path):
     """tinyrender_amd <scene.toml> (src/main.cpp:121-181 on the GPU path): the
     reference's own scene file shape (cbox_bdpt_glass.toml with the film and spp
@@ -290,6 +295,24 @@ def test_gpu_path_tracer_matches_reference_golden(name, golden_manifest):
     worst, exact, whole = report(fb, ref)
     assert np.all(np.isfinite(fb))
     assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact floats {exact:.4f}, image {whole:.3g})"
+
+
+def test_gpu_path_tracer_render_device_and_level_check(golden_manifest):
+    """The asynchronous path-tracer entry bench.py uses (device framebuffer, the
+    caller's stream), then check_levels() after the sync: same frame as the golden."""
+    import torch
+
+    name = sorted(golden_manifest["path_framebuffers"])[0]
+    m = golden_manifest["path_framebuffers"][name]
+    cam = bdpt_amd.Camera(**variants.SCENES[m["scene"]]["camera"])
+    cfg = bdpt_amd.Config(camera=cam, width=m["width"], height=m["height"], spp=m["spp"])
+    it = bdpt_amd.PathTracerIntegrator(scene(m["scene"]), cfg, bdpt_amd.PathSettings(**m["path"]))
+    fb = torch.zeros(m["width"] * m["height"] * 3, dtype=torch.float32, device="cuda:0")
+    s = torch.cuda.Stream()
+    it.render_device(fb.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    it.check_levels()
+    assert rel_l2(fb.cpu().numpy(), load_golden(name)).max() <= TOL
 
 
 def test_gpu_path_tracer_long_paths_match_oracle():

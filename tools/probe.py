@@ -15,7 +15,7 @@ sc = variants.SCENES[name]
 cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**sc["camera"]), width=W, height=H, spp=spp, rr_depth=sc["rr_depth"])
 it = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(name)), cfg)
 it.init()
-xf = int(os.environ.get("PROBE_FLAGS", "0"))  # e.g. 4 = wavefront schedule
+xf = int(os.environ.get("PROBE_FLAGS", "0"))  # e.g. 1 = counting pass
 it.render_frame(flags=xf)
 it.render_frame(flags=xf)
 t_plain = it.stats()["kernel_ms"]
