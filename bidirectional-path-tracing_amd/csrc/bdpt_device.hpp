@@ -942,6 +942,15 @@ __device__ __forceinline__ Ray shadow_ray(f3 start, f3 end) {
 // -------------------------------------------------------------------- BSDFs
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 
+#ifndef BDPT_GLOSSY_ATTR
+#define BDPT_GLOSSY_ATTR __forceinline__  // the Phong-bearing eval / pdf (measured: inline +2 %)
+#endif
+#ifndef BDPT_EVAL_PDFS
+#define BDPT_EVAL_PDFS 0  // 1: connections share one powf per BSDF (measured slower: 190.8 vs 195.9)
+#endif
+#ifndef BDPT_SAMPLE_ATTR
+#define BDPT_SAMPLE_ATTR BDPT_NOINLINE  // the non-diffuse BSDF samplers out of line
+#endif
 // MixtureBSDF::eval == PhongBSDF::eval (mixture.h:59-75, phong.h:56-71).
 // With Ks == 0 the specular term is (0 * (n + 2)) * INV_TWOPI * powf(c, n) = +0
 // (powf of c in [0, 1] is finite), and val + 0 == val: skipping it is exact.
@@ -960,7 +969,7 @@ __device__ __forceinline__ f3 glossy_eval(const BsdfRecord& b, f3 wi, f3 wo) {
     return val;
 }
 
-__device__ BDPT_NOINLINE f3 glossy_eval_call(const BsdfRecord& b, f3 wi, f3 wo) { return glossy_eval(b, wi, wo); }
+__device__ BDPT_GLOSSY_ATTR f3 glossy_eval_call(const BsdfRecord& b, f3 wi, f3 wo) { return glossy_eval(b, wi, wo); }
 
 // BSDF::eval. The diffuse and delta lobes are a few instructions and stay
 // inline; only the Phong-bearing lobes (powf) go through a call.
@@ -983,7 +992,7 @@ __device__ __forceinline__ float phong_part_pdf(const BsdfRecord& b, f3 wi, f3 w
 
 // With specw == 0, pdfPhong * 0 = +0 (pdfPhong is finite and >= 0) and
 // 0 + pdfDiffuse * (1 - 0) == pdfDiffuse: skipping the Phong lobe is exact.
-__device__ BDPT_NOINLINE float glossy_pdf_call(const BsdfRecord& b, f3 wi, f3 wo) {
+__device__ BDPT_GLOSSY_ATTR float glossy_pdf_call(const BsdfRecord& b, f3 wi, f3 wo) {
     if (b.kind == BSDF_MIXTURE) {  // mixture.h:78-100
         const float pd = cosine_hemisphere_pdf(wi);
         const float pp = phong_part_pdf(b, wi, wo);
@@ -997,6 +1006,60 @@ __device__ __forceinline__ float bsdf_pdf(const BsdfRecord& b, f3 wi, f3 wo) {
         return cosine_hemisphere_pdf(wi);
     if (kind == BSDF_MIXTURE || kind == BSDF_PHONG) return glossy_pdf_call(b, wi, wo);
     return 0.f;
+}
+
+// eval(wi, wo), pdf(wi, wo) and pdf(wo, wi) of one BSDF — what every
+// connection needs at each end (bdpt.h:374-483) — with ONE powf for the Phong
+// lobe: the cosine of eval (dot(wi, reflect(wo)), clamped to [0, 1]) and the
+// lobe's local z in both pdfs (Frame(reflect(wo)).toLocal(wi).z = dot(wi,
+// reflect(wo)), and dot(wo, reflect(wi)) has the same products in the same
+// order) are one value z. eval takes powf(clamp(z)), the pdfs powf(z) for
+// z >= 0: the same call unless z > 1, where eval's powf(1, n) is exactly 1.
+// Each output is bit-identical to bsdf_eval / bsdf_pdf above.
+struct EvalPdfs {
+    f3 f;
+    float fwd, rev;  // pdf(wi, wo), pdf(wo, wi)
+};
+__device__ __forceinline__ EvalPdfs bsdf_eval_pdfs(const BsdfRecord& b, f3 wi, f3 wo) {
+#if BDPT_EVAL_PDFS
+    EvalPdfs r{mk(0.f, 0.f, 0.f), 0.f, 0.f};
+    const int kind = b.kind;
+    if (kind == BSDF_DIFFUSE) {
+        if (wi.z >= 0.f && wo.z >= 0.f) r.f = (ld3(b.kd) * kInvPi) * wi.z;
+        r.fwd = cosine_hemisphere_pdf(wi);
+        r.rev = cosine_hemisphere_pdf(wo);
+        return r;
+    }
+    if (kind != BSDF_MIXTURE && kind != BSDF_PHONG) return r;  // delta lobes
+    const float ex = b.exponent;
+    const float z = dot(wi, reflect_z(wo));
+    const bool eval_on = wi.z >= 0.f && wo.z >= 0.f;
+    const bool ks_on = b.ks[0] != 0.f || b.ks[1] != 0.f || b.ks[2] != 0.f;
+    const bool lobe_pdf = kind == BSDF_PHONG || b.specw != 0.f;
+    float pw = 0.f;
+    if ((eval_on && ks_on) || (lobe_pdf && z >= 0.f))
+        pw = glibc_powf(z > 1.f ? z : glibc_fminf(glibc_fmaxf(z, 0.f), 1.f), ex);
+    if (eval_on) {  // glossy_eval
+        f3 val = mk(0.f, 0.f, 0.f);
+        val = val + ld3(b.kd) * kInvPi;
+        if (ks_on) val = val + ((ld3(b.ks) * (ex + 2)) * kInvTwoPi) * (z > 1.f ? 1.f : pw);
+        val = val * b.scale;
+        r.f = val * wi.z;
+    }
+    const float pp = z >= 0.f ? (ex + 2) * kInvTwoPi * pw : 0.f;  // phong_lobe_pdf
+    if (kind == BSDF_PHONG) {
+        r.fwd = r.rev = pp;
+    } else if (b.specw == 0.f) {
+        r.fwd = cosine_hemisphere_pdf(wi);
+        r.rev = cosine_hemisphere_pdf(wo);
+    } else {
+        r.fwd = (pp * b.specw) + (cosine_hemisphere_pdf(wi) * (1.f - b.specw));
+        r.rev = (pp * b.specw) + (cosine_hemisphere_pdf(wo) * (1.f - b.specw));
+    }
+    return r;
+#else
+    return EvalPdfs{bsdf_eval(b, wi, wo), bsdf_pdf(b, wi, wo), bsdf_pdf(b, wo, wi)};
+#endif
 }
 
 // glass.h:40-53
@@ -1080,7 +1143,7 @@ struct BsdfSample {
     f3 f, wi;
     float pdf;
 };
-__device__ BDPT_NOINLINE BsdfSample bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u) {
+__device__ BDPT_SAMPLE_ATTR BsdfSample bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u) {
     BsdfSample s;
     s.f = bsdf_sample_body(b, wo, u, s.wi, s.pdf);
     return s;

@@ -403,10 +403,11 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const float cosAtEye = wi.z;
         if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
         const float pdf_w = div_cr((e_pdf * e_pos_pdf) * d2, cosAtLight);
-        const f3 Li = ((bsdf_eval(b, wi, L.h.wo) * rcp_cr(pdf_w)) * L.c.tp) * ld3(e.radiance);
+        const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
+        const f3 Li = ((ep.f * rcp_cr(pdf_w)) * L.c.tp) * ld3(e.radiance);
         if (is_zero(Li)) break;
-        const float lightWeight = div_cr(bsdf_pdf(b, wi, L.h.wo) * 1.f, pdf_w);
-        const float eyePrevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;
+        const float lightWeight = div_cr(ep.fwd * 1.f, pdf_w);
+        const float eyePrevRev = ep.rev * 1.f;
         const float eyeCurRev_a = cosAtEye * rcp_cr(d2) * kInvTwoPi;
         const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
         const float mis = rcp_cr(lightWeight + 1.f + eyeWeight);
@@ -433,7 +434,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const float cosCamera = dot(fwd, e2l);
         if (cosCamera <= 0.f) break;
         const f3 wi = local_at(L.h.n, -e2l);
-        const f3 f = bsdf_eval(b, wi, L.h.wo);
+        const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
+        const f3 f = ep.f;
         if (is_zero(f) || wi.z <= 0.f) break;
         const float d = div_cr(fr.cam.vnear, cosCamera);
         const float img2solid = div_cr(d * d, cosCamera);
@@ -445,7 +447,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         rad = rad * rcp_cr(nlight);
         rad = rad * rcp_cr(static_cast<float>(fr.spp));
         const float reversePdf_a = 1.f * img2surf;
-        const float prevRev = bsdf_pdf(b, L.h.wo, wi) * 1.f;  // swapped (wi, wo), rr = 1
+        const float prevRev = ep.rev * 1.f;  // swapped (wi, wo), rr = 1
         const float lightWeight = div_cr(reversePdf_a, nlight) * (L.c.vcm + prevRev * L.c.vc);
         const float mis = rcp_cr(lightWeight + 1.f + 0.f);
         L.c.pend = (fr.strategy == 0) ? rad * mis : rad;
@@ -472,12 +474,13 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 continue;
             }
             const BsdfRecord& bl = bsdf_of(sc, V.mat);
-            f3 Li = bsdf_eval(bl, wiL, V.wo) * bsdf_eval(be, wiE, L.h.wo);
+            const EvalPdfs eL = bsdf_eval_pdfs(bl, wiL, V.wo), eE = bsdf_eval_pdfs(be, wiE, L.h.wo);
+            f3 Li = eL.f * eE.f;
             Li = Li * ((V.tp * L.c.tp) * invD2);
-            const float eyePathRev_w = bsdf_pdf(bl, wiL, V.wo) * 1.f;  // * vertex rr (1)
-            const float lightPrevRev = bsdf_pdf(bl, V.wo, wiL) * 1.f;
-            const float lightPathRev_w = bsdf_pdf(be, wiE, L.h.wo) * 1.f;
-            const float eyePrevRev = bsdf_pdf(be, L.h.wo, wiE) * 1.f;
+            const float eyePathRev_w = eL.fwd * 1.f;  // * vertex rr (1)
+            const float lightPrevRev = eL.rev * 1.f;
+            const float lightPathRev_w = eE.fwd * 1.f;
+            const float eyePrevRev = eE.rev * 1.f;
             const float lightPathRev_a = lightPathRev_w * cosL * invD2;
             const float eyePathRev_a = eyePathRev_w * cosE * invD2;
             const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);

@@ -213,44 +213,54 @@ __device__ BDPT_NOINLINE float glibc_sincosf(float y, int which) {
     }
     return sincos_poly(x * s, x * x, sincos_poly_table(neg), which ? (n ^ 1) : n);
 }
-// sinf(y) and cosf(y) from one range reduction: each output is bit-identical
-// to the corresponding single call above (same reduction, same polynomial).
+
 struct SinCos {
     float s, c;
 };
 #ifndef BDPT_SINCOS_ATTR
-#define BDPT_SINCOS_ATTR BDPT_NOINLINE  // out of line: the megakernel's registers are not sized for it
+#define BDPT_SINCOS_ATTR __forceinline__  // branch-free below 120: inline costs fewer registers than a call
 #endif
-__device__ BDPT_SINCOS_ATTR SinCos glibc_sincosf2(float y) {
-    double x = y;
-    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
-        double x2 = x * x;
-        if (abstop12(y) < abstop12(0x1p-12f)) return SinCos{y, 1.0f};
-        const SinCosPoly p = sincos_poly_table(false);
-        return SinCos{sincos_poly(x, x2, p, 0), sincos_poly(x, x2, p, 1)};
-    }
-    int n;
-    double s;
-    bool neg;
-    if (abstop12(y) < abstop12(120.0f)) {
-        double r = x * 0x1.45f306dc9c883p+23;
-        n = (static_cast<int32_t>(r) + 0x800000) >> 24;
-        x = __builtin_fma(-static_cast<double>(n), 0x1.921fb54442d18p+0, x);
-        s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
-        neg = (n & 2) != 0;
-    } else if (abstop12(y) < abstop12(__builtin_inff())) {
-        uint32_t xi = f2u(y);
-        int sign = xi >> 31;
-        x = sincos_reduce_large(xi, &n);
-        int q = n + sign;
-        s = ((q & 3) == 1 || (q & 3) == 2) ? -1.0 : 1.0;
-        neg = (q & 2) != 0;
-    } else {
+// |y| >= 120, inf, NaN: reduce_large (never reached by the warps' angles).
+__device__ __noinline__ SinCos glibc_sincosf2_large(float y) {
+    if (abstop12(y) >= abstop12(__builtin_inff())) {
         const float nan = (y - y) / (y - y);
         return SinCos{nan, nan};
     }
-    const SinCosPoly p = sincos_poly_table(neg);
+    int n;
+    const uint32_t xi = f2u(y);
+    const int sign = xi >> 31;
+    const double x = sincos_reduce_large(xi, &n);
+    const int q = n + sign;
+    const double s = ((q & 3) == 1 || (q & 3) == 2) ? -1.0 : 1.0;
+    const SinCosPoly p = sincos_poly_table((q & 2) != 0);
     return SinCos{sincos_poly(x * s, x * x, p, n), sincos_poly(x * s, x * x, p, n ^ 1)};
+}
+// sinf(y) and cosf(y) from one range reduction, each bit-identical to the
+// single calls above, without divergent branches for |y| < 120 (every angle the
+// warps produce): glibc's reduce_fast path, with both polynomials evaluated once
+// and assigned by the quadrant's parity. It also covers glibc's two small-
+// argument paths: for |y| < pi/4 the reduction gives n = 0 and x = y exactly
+// (the same polynomial call), and for |y| < 2^-12 both polynomials round to
+// glibc's (y, 1.0f) (the terms past x / 1 are below half an ulp; only the sign
+// of a zero sine needs the explicit select). A negated
+// cosine table negates the polynomial's value exactly (fma is sign-symmetric
+// under round-to-nearest), so the quadrant's sign is applied to the float.
+// tools/numerics/sincos_check.hip compares it with the branchy form over every
+// float with |y| < 120.
+__device__ BDPT_SINCOS_ATTR SinCos glibc_sincosf2(float y) {
+    if (abstop12(y) >= abstop12(120.0f)) return glibc_sincosf2_large(y);
+    double x = y;
+    const double r = x * 0x1.45f306dc9c883p+23;
+    const int n = (static_cast<int32_t>(r) + 0x800000) >> 24;
+    x = __builtin_fma(-static_cast<double>(n), 0x1.921fb54442d18p+0, x);
+    const double xs = ((n & 3) == 1 || (n & 3) == 2) ? -x : x;
+    const double x2 = x * x;
+    const SinCosPoly p = sincos_poly_table(false);
+    float sp = sincos_poly(xs, x2, p, 0);  // sine polynomial
+    sp = (y == 0.f) ? y : sp;              // sinf(-0) = -0 (glibc's tiny-argument path)
+    float cp = sincos_poly(xs, x2, p, 1);        // cosine polynomial
+    cp = (n & 2) ? -cp : cp;
+    return (n & 1) ? SinCos{cp, sp} : SinCos{sp, cp};
 }
 
 __device__ __forceinline__ float glibc_sinf(float x) { return glibc_sincosf(x, 0); }
@@ -348,7 +358,10 @@ __device__ __noinline__ float powf_special(float x, float y, uint32_t ix, uint32
     return 0.f;
 }
 
-__device__ BDPT_NOINLINE float glibc_powf(float x, float y) {
+#ifndef BDPT_POWF_ATTR
+#define BDPT_POWF_ATTR BDPT_NOINLINE
+#endif
+__device__ BDPT_POWF_ATTR float glibc_powf(float x, float y) {
     uint32_t sign_bias = 0;
     uint32_t ix = f2u(x), iy = f2u(y);
     if (ix - 0x00800000 >= 0x7f800000 - 0x00800000 || powf_zeroinfnan(iy)) {

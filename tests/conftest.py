@@ -2,6 +2,11 @@ import os
 import sys
 
 import pytest
+# torch before the product library in every test process (as bench.py and
+# INTEGRATION.md do): both link SONAME libamdhip64.so.7, and whichever loads
+# first is the HIP runtime the other binds to; tests that hand torch tensors and
+# streams to the library need torch's.
+import torch  # noqa: F401
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for sub in ("", "oracle", "scenes", "bidirectional-path-tracing_amd"):
