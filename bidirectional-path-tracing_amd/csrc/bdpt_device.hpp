@@ -333,6 +333,21 @@ __device__ __forceinline__ f3 uniform_hemisphere(F2 u) {
 __device__ __forceinline__ f3 cosine_hemisphere(F2 u) {
     float rx = (2.f * u.x) - 1.f;
     float ry = (2.f * u.y) - 1.f;
+#ifndef BDPT_DISK_SELECT
+#define BDPT_DISK_SELECT 1
+#endif
+#if BDPT_DISK_SELECT
+    // Both branches of the reference as selects (one division, one sincos per
+    // lane, same operations and bits); the (0, 0) sample keeps dx = dy = 0.
+    const bool zero = rx == 0 && ry == 0;
+    const bool xb = (rx * rx) > (ry * ry);
+    const float radius = xb ? rx : ry;
+    const float q = (kPi * 0.25f) * ((xb ? ry : rx) * rcp_cr(xb ? rx : ry));
+    const float phi = zero ? 0.f : (xb ? q : (kPi * 0.5f) - q);
+    const SinCos sc = glibc_sincosf2(phi);
+    const float dx = zero ? 0.f : radius * sc.c;
+    const float dy = zero ? 0.f : radius * sc.s;
+#else
     float dx = 0.f, dy = 0.f;
     if (!(rx == 0 && ry == 0)) {
         float radius, phi;
@@ -347,6 +362,7 @@ __device__ __forceinline__ f3 cosine_hemisphere(F2 u) {
         dx = radius * sc.c;
         dy = radius * sc.s;
     }
+#endif
     float z = 1.0f - (dx * dx + dy * dy);
     z = glibc_fmaxf(z, 0.f);
     return mk(dx, dy, sqrt_cr(z));
@@ -371,7 +387,17 @@ __device__ __forceinline__ F2 uniform_triangle(F2 s) {
 
 // -------------------------------------------------------------------- frame
 // Frame(n) with coordinateSystem (core.h:155-157, math.h:42-51): t = c, s = cross(c, n).
+#ifndef BDPT_FRAME_SELECT
+#define BDPT_FRAME_SELECT 0  // 1: the operand selected first, one sqrt + division per lane
+#endif
 __device__ __forceinline__ void make_frame(f3 a, f3& s, f3& t) {
+#if BDPT_FRAME_SELECT
+    const bool xb = fabsf(a.x) > fabsf(a.y);
+    const float u = xb ? a.x : a.y;
+    const float inv = rcp_cr(sqrt_cr(u * u + a.z * a.z));
+    const float w = a.z * inv, m = -u * inv;
+    t = xb ? mk(w, 0.f, m) : mk(0.f, w, m);
+#else
     if (fabsf(a.x) > fabsf(a.y)) {
         float inv = rcp_cr(sqrt_cr(a.x * a.x + a.z * a.z));
         t = mk(a.z * inv, 0.f, -a.x * inv);
@@ -379,6 +405,7 @@ __device__ __forceinline__ void make_frame(f3 a, f3& s, f3& t) {
         float inv = rcp_cr(sqrt_cr(a.y * a.y + a.z * a.z));
         t = mk(0.f, a.z * inv, -a.y * inv);
     }
+#endif
     s = cross(t, a);
 }
 __device__ __forceinline__ f3 to_local(f3 s, f3 t, f3 n, f3 v) { return mk(dot(v, s), dot(v, t), dot(v, n)); }
