@@ -8,7 +8,7 @@ cd "$(dirname "$0")/../bidirectional-path-tracing_amd"
 NAME=$1; shift
 O=lib/obj_$NAME
 mkdir -p $O
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I../include -Icsrc"
+F="--offload-arch=gfx950 ${OPT:--O3} -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I../include -Icsrc"
 /opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/bdpt_kernels.hip -o $O/k.o
 OTHERS=$(ls lib/obj/*.o | grep -v -e '/bdpt_kernels.o$' -e '/tinyrender_main.o$')
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $O/k.o $OTHERS -ldl -o lib/libbdpt_amd_$NAME.so
