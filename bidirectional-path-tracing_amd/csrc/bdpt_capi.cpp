@@ -45,6 +45,11 @@ hipError_t launch_frame_deep(const dev::DevScene& sc, const dev::DevFrame& fr, f
                              uint2* gstack, uint32_t nslots, unsigned long long* work, unsigned long long* counters,
                              int grid, hipStream_t stream, void* dparams);
 int frame_kernel_blocks_per_cu_deep(size_t dyn_lds);
+// bdpt_kernels_hbm.hip: the same megakernel with the BSDF records in HBM
+hipError_t launch_frame_hbm(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                            uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
+                            hipStream_t stream, void* dparams);
+int frame_kernel_blocks_per_cu_hbm(size_t dyn_lds);
 size_t pt_params_bytes();
 int pt_blocks_per_cu(size_t dyn_lds);
 hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8], float* fb,
@@ -334,25 +339,35 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     c->sc.nshapes = static_cast<int32_t>(L.shape_emitter.size());
     {  // LDS table layout (bdpt_device.hpp scene_tables_to_lds), 16-byte aligned parts
         auto up4 = [](uint32_t w) { return (w + 3u) & ~3u; };
+        constexpr uint32_t kBudget = 24u * 1024u;
         const uint32_t nb = static_cast<uint32_t>(L.bsdfs.size() * sizeof(BsdfRecord) / 4);
-        c->sc.lds_emit_off = up4(dev::kLdsHdr + nb);
-        c->sc.lds_shape_off = up4(c->sc.lds_emit_off + static_cast<uint32_t>(L.emitters.size() * sizeof(EmitterRecord) / 4));
+        const uint32_t ne = static_cast<uint32_t>(L.emitters.size() * sizeof(EmitterRecord) / 4);
+        // BSDF records in LDS unless they do not fit with the emitter records (then
+        // the frame renders run bdpt_kernels_hbm.hip); BDPT_BSDF_IN_HBM=1 forces
+        // HBM (tests of that build on small scenes).
+        const char* force = std::getenv("BDPT_BSDF_IN_HBM");
+        const bool hbm = (force && *force == '1') || (up4(up4(dev::kLdsHdr + nb) + ne) * 4u > kBudget);
+        c->sc.lds_bsdf_off = hbm ? dev::kNoLds : dev::kLdsHdr;
+        c->sc.lds_emit_off = hbm ? dev::kLdsHdr : up4(dev::kLdsHdr + nb);
+        c->sc.lds_shape_off = up4(c->sc.lds_emit_off + ne);
         c->sc.lds_words = up4(c->sc.lds_shape_off + static_cast<uint32_t>(L.shape_emitter.size()));
-        if (c->sc.lds_words * 4u > 24u * 1024u) {  // many shapes: their emitter map stays in HBM
+        if (c->sc.lds_words * 4u > kBudget) {  // many shapes: their emitter map stays in HBM
             c->sc.lds_words = c->sc.lds_shape_off;
             c->sc.lds_shape_off = dev::kNoLds;
         }
-        if (c->sc.lds_words * 4u > 24u * 1024u)
-            return fail(BDPT_ERR_UNSUPPORTED, "BSDF / emitter tables exceed the 24 KiB LDS budget");
+        if (c->sc.lds_words * 4u > kBudget)
+            return fail(BDPT_ERR_UNSUPPORTED, "emitter records exceed the 24 KiB LDS budget");
         // Emitter faces + CDFs join the LDS tables when that costs no resident block.
         c->sc.lds_etri_off = c->sc.lds_ecdf_off = dev::kNoLds;
         c->sc.n_etri = static_cast<int32_t>(L.emit_tri.size() / 5);
         c->sc.n_ecdf = static_cast<int32_t>(L.emit_cdf.size());
         const uint32_t etri = c->sc.lds_words, ecdf = up4(etri + 20u * static_cast<uint32_t>(c->sc.n_etri));
         const uint32_t with = up4(ecdf + static_cast<uint32_t>(c->sc.n_ecdf));
-        if (with * 4u <= 24u * 1024u &&
-            frame_kernel_blocks_per_cu(4 * static_cast<size_t>(with)) >=
-                frame_kernel_blocks_per_cu(4 * static_cast<size_t>(c->sc.lds_words))) {
+        auto blocks = [&](uint32_t words) {
+            const size_t bytes = 4 * static_cast<size_t>(words);
+            return hbm ? frame_kernel_blocks_per_cu_hbm(bytes) : frame_kernel_blocks_per_cu(bytes);
+        };
+        if (with * 4u <= kBudget && blocks(with) >= blocks(c->sc.lds_words)) {
             c->sc.lds_etri_off = etri;
             c->sc.lds_ecdf_off = ecdf;
             c->sc.lds_words = with;
@@ -365,7 +380,9 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     HIP_TRY(hipMalloc(&c->dparams, frame_params_bytes()));
     // Persistent grid: exactly the resident blocks (no co-residency is assumed:
     // the work queue has no inter-block waits, extra blocks would just queue).
-    c->grid = c->cus * frame_kernel_blocks_per_cu(4 * static_cast<size_t>(c->sc.lds_words));
+    const size_t dyn = 4 * static_cast<size_t>(c->sc.lds_words);
+    c->grid = c->cus * (c->sc.lds_bsdf_off == dev::kNoLds ? frame_kernel_blocks_per_cu_hbm(dyn)
+                                                          : frame_kernel_blocks_per_cu(dyn));
     c->nslots = static_cast<uint32_t>(c->grid * frame_kernel_block());
     // Traversal stack: worst case of either tree (binary: depth + 1 pending
     // right children; 4-wide: the host-computed bound), the part beyond the
@@ -422,6 +439,10 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const dev::DevFrame fr = make_frame(p);
+    const bool hbm = c->sc.lds_bsdf_off == dev::kNoLds;
+    if (hbm && p->rr_depth > kLazyRrDepth)
+        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 with BSDF records in HBM (too many materials for the LDS "
+                                          "table) is not built");
     if ((rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
     dev::DevScene sc = c->sc;
     if (p->rr_depth > kLazyRrDepth) {  // draws past 226: the lanes' MT19937 rings
@@ -440,6 +461,9 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
                                                            4 * static_cast<size_t>(c->sc.lds_words)));
             HIP_TRY(launch_frame_deep(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
                                       c->dparams));
+        } else if (hbm) {
+            HIP_TRY(launch_frame_hbm(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
+                                     c->dparams));
         } else {
             HIP_TRY(launch_frame(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
                                  c->dparams));
@@ -459,6 +483,14 @@ static int ensure_tmp_fb(bdpt_ctx* c, size_t floats);
 
 // PathTracerIntegrator (path.h) on the same substrate: pt_kernels.hip.
 constexpr int kPtMaxLevels = 512;  // recursion levels per lane under Russian roulette (P(> 512) ~ 0.95^507)
+
+// The path / direct frame kernels read the BSDF records from the LDS table only.
+static int pt_frame_tables(const bdpt_ctx* c) {
+    if (c->sc.lds_bsdf_off == dev::kNoLds)
+        return fail(BDPT_ERR_UNSUPPORTED, "the path / direct frame renders need the BSDF records in the LDS table "
+                                          "(too many materials; bdpt_render and the single-sample calls take them)");
+    return BDPT_OK;
+}
 
 static int ensure_pt(bdpt_ctx* c, int levels) {
     if (!c->pt_dparams) {
@@ -499,7 +531,7 @@ int bdpt_render_path(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_pa
     if (levels > kPtMaxLevels) return fail(BDPT_ERR_UNSUPPORTED, "maxDepth > 510 is not supported");
     HIP_TRY(hipSetDevice(c->device));
     int rc;
-    if ((rc = ensure_pt(c, levels))) return rc;
+    if ((rc = pt_frame_tables(c)) || (rc = ensure_pt(c, levels))) return rc;
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const dev::DevFrame fr = make_frame(p);
     int32_t settings[8] = {path->is_explicit ? 1 : 0, path->max_depth, path->rr_depth, 0, path->emitter_samples,
@@ -553,7 +585,7 @@ int bdpt_render_direct(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direc
     if (d->emitter_samples < 0 || d->bsdf_samples < 0) return fail(BDPT_ERR_INVALID, "negative sample counts");
     HIP_TRY(hipSetDevice(c->device));
     int rc;
-    if ((rc = ensure_pt(c, 1))) return rc;
+    if ((rc = pt_frame_tables(c)) || (rc = ensure_pt(c, 1))) return rc;
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const dev::DevFrame fr = make_frame(p);
     const int32_t settings[8] = {1, -1, 0, 0, d->emitter_samples, d->bsdf_samples, 1, d->sampling_strategy};

@@ -54,6 +54,7 @@ struct DevScene {
     // LDS copy of the small tables (scene_tables_to_lds): word offsets of the
     // emitter records and the shape->emitter map, total words (16-byte rounded)
     uint32_t lds_emit_off, lds_shape_off, lds_words;
+    uint32_t lds_bsdf_off;  // kLdsHdr, or kNoLds: the BSDF records stay in HBM (too many materials)
     // emitter faces (5 float4 each) and CDFs, also in LDS when they fit without
     // costing a resident block (host decision); kNoLds otherwise
     uint32_t lds_etri_off, lds_ecdf_off;
@@ -73,8 +74,23 @@ constexpr uint32_t kLdsHdr = 4;  // LDS header words: mt_ring (2 words), mt_ring
 // [shape_off, ...) int32 shape_emitter[nshapes] (unless kNoLds); anything a kernel keeps in
 // dynamic LDS besides goes at lds_words.
 extern __shared__ uint32_t g_scene_lds[];
-__device__ __forceinline__ const BsdfRecord& bsdf_of(const DevScene&, int m) {
+// Where the BSDF records are read: 0 = the LDS table only (the frame kernels'
+// default build), 1 = HBM only (bdpt_kernels_hbm.hip: scenes whose records do not
+// fit the LDS budget), 2 = chosen per launch by sc.lds_bsdf_off (the single-
+// sample and per-function kernels: a generic pointer, flat loads — measured 8 %
+// slower in the frame kernel, irrelevant for one wave).
+#ifndef BDPT_BSDF_TABLE
+#define BDPT_BSDF_TABLE 2
+#endif
+__device__ __forceinline__ const BsdfRecord& bsdf_of(const DevScene& sc, int m) {
+#if BDPT_BSDF_TABLE == 1
+    return sc.bsdf[m];
+#else
+#if BDPT_BSDF_TABLE == 2
+    if (sc.lds_bsdf_off == kNoLds) return sc.bsdf[m];
+#endif
     return reinterpret_cast<const BsdfRecord*>(g_scene_lds + kLdsHdr)[m];
+#endif
 }
 __device__ __forceinline__ const EmitterRecord& emitter_of(const DevScene& sc, int i) {
     return reinterpret_cast<const EmitterRecord*>(g_scene_lds + sc.lds_emit_off)[i];
@@ -99,7 +115,8 @@ __device__ __forceinline__ void scene_tables_to_lds(const DevScene& sc) {
         g_scene_lds[2] = sc.mt_ring_stride;
         g_scene_lds[3] = 0u;
     }
-    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) g_scene_lds[kLdsHdr + i] = b[i];
+    if (sc.lds_bsdf_off != kNoLds)
+        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) g_scene_lds[kLdsHdr + i] = b[i];
     for (uint32_t i = threadIdx.x; i < ne; i += blockDim.x) g_scene_lds[sc.lds_emit_off + i] = e[i];
     if (sc.lds_shape_off != kNoLds)
         for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(sc.nshapes); i += blockDim.x)

@@ -20,6 +20,14 @@
 // one lane).
 #include <hip/hip_runtime.h>
 
+#ifndef BDPT_BSDF_TABLE
+#if BDPT_SAMPLER_STATE
+#define BDPT_BSDF_TABLE 2  // one wave: the table's place is chosen per launch
+#else
+#define BDPT_BSDF_TABLE 0  // frame kernels: LDS (bdpt_kernels_hbm.hip is the HBM build)
+#endif
+#endif
+
 #include "bdpt_path.hpp"
 
 namespace bdpt {

@@ -19,6 +19,9 @@
 
 #include <cstring>
 
+#ifndef BDPT_BSDF_TABLE
+#define BDPT_BSDF_TABLE 0  // the path / direct frame kernels read the LDS table only
+#endif
 #include "bdpt_path.hpp"
 
 namespace bdpt {

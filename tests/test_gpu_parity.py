@@ -129,6 +129,51 @@ def test_gpu_rr_depth_limits():
         it.render_frame()
 
 
+def test_gpu_many_materials_take_the_hbm_table_build(tmp_path):
+    """408 materials: the BSDF records (72 B each) outgrow the 24 KiB LDS table,
+    so bdpt_render runs the HBM-table build of the megakernel and the single-
+    sample kernel reads them from HBM per launch — same frame and sample as the
+    oracle. The path / direct frame kernels (LDS table only) and rrDepth > 28
+    (no deep HBM build) refuse such a scene instead of rendering it wrong."""
+    obj = variants.many_materials_obj(str(tmp_path))
+    cam = variants.SCENES["cbox_low"]["camera"]
+    W, H, spp, rr = 32, 24, 4, 5
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**cam), width=W, height=H, spp=spp, rr_depth=rr)
+    sc = bdpt_amd.Scene(obj)
+    assert sc.info()["materials"] == 408
+    fb = bdpt_amd.BDPTIntegrator(sc, cfg).render_frame().reshape(-1)
+    osc = O.Scene(obj)
+    p = O.make_params(cam, W, H, spp, rr)
+    ref, _ = osc.render(p)
+    worst, exact, _ = report(fb, ref.reshape(-1))
+    assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
+    it = bdpt_amd.BDPTIntegrator(sc, cfg)
+    it.init()
+    for pixel, k in [(300, 1), (500, 3)]:
+        it.rgb[:] = 0
+        Li_ref, splats_ref = osc.sample(p, pixel, k)
+        ray, sampler = driver_ray(p, "cbox_low", pixel, k)
+        assert np.allclose(it.render(ray, sampler), Li_ref, rtol=1e-6, atol=0)
+        assert rel_l2(it.rgb.reshape(-1), splats_ref).max() <= TOL
+    with pytest.raises(bdpt_amd.BdptError, match="LDS table"):
+        bdpt_amd.PathTracerIntegrator(sc, cfg).render_frame()
+    deep = bdpt_amd.Config(camera=bdpt_amd.Camera(**cam), width=8, height=8, spp=1, rr_depth=29)
+    with pytest.raises(bdpt_amd.BdptError, match="rr_depth"):
+        bdpt_amd.BDPTIntegrator(sc, deep).render_frame()
+
+
+@pytest.mark.parametrize("name", ["G1_cbox_low_64x64_spp4", "G2_caustic_64x64_spp16"])
+def test_gpu_hbm_table_build_matches_golden(name, golden_manifest, monkeypatch):
+    """The HBM-table build forced on a small scene (BDPT_BSDF_IN_HBM=1 at context
+    creation): the reference's frame."""
+    monkeypatch.setenv("BDPT_BSDF_IN_HBM", "1")
+    m = golden_manifest["framebuffers"][name]
+    it = integrator(m["scene"], m["width"], m["height"], m["spp"], m["rr_depth"], STRATEGY[m.get("strategy", "bdpt")])
+    fb = it.render_frame(row_offset=0, row_stride=m["row_stride"]).reshape(-1)
+    worst, exact, _ = report(fb, load_golden(name))
+    assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact floats {exact:.4f})"
+
+
 def test_gpu_camera_facing_away_renders_black():
     cam = dict(variants.SCENES["caustic"]["camera"])
     cam["at"] = [0.0, 0.8, 10.0]

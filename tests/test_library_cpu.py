@@ -140,3 +140,16 @@ def test_sampler_state_is_std_mt19937():
         st = np.zeros(bdpt_amd.MT19937_WORDS, np.uint32)
         assert bdpt_amd.lib().bdpt_sampler_state(seed, draws, ctypes.c_void_p(st.ctypes.data)) == 0
         assert np.array_equal(st, py.state), (seed, draws)
+
+
+def test_ingest_matches_oracle_with_many_materials(tmp_path):
+    """408 materials (every BSDF kind): product ingest == oracle ingest, and the
+    BSDF types the scene's illum values map to (diffuse / mixture / mirror / glass)."""
+    import oracle as O
+    obj = variants.many_materials_obj(str(tmp_path))
+    s = bdpt_amd.Scene(obj)
+    for x, y in zip(s.export(), O.Scene(obj).dump()):
+        assert np.array_equal(x, y)
+    assert s.info()["materials"] == 408
+    kinds = {s.bsdf_type(i)[1] for i in range(408)}
+    assert kinds == {1, 2, 3, 4}
