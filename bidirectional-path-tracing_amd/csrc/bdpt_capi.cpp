@@ -113,6 +113,8 @@ struct bdpt_ctx {
     std::vector<void*> allocs;
     dev::DevScene sc{};
     int max_depth = 0;
+    bool tri_tree = false;              // traversal boxes padded (wide_bvh.hpp kTriBoxPad)
+    double box_lo[3] = {}, box_hi[3] = {};  // scene bounds (the reference BVH's root box)
     int64_t scene_bytes = 0;
     // work buffers
     unsigned long long* work = nullptr;      // work counter
@@ -332,6 +334,9 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     if ((rc = upload(c.get(), L.shape_emitter.data(), L.shape_emitter.size() * 4, &p))) return rc;
     c->sc.shape_emitter = static_cast<const int32_t*>(p);
     c->sc.root_link = L.root_link;
+    c->sc.node_slack = 1u;  // per render: node_slack_needed
+    c->tri_tree = L.tri_tree;
+    for (int a = 0; a < 3; a++) c->box_lo[a] = s->host.nodes[0].bmin[a], c->box_hi[a] = s->host.nodes[0].bmax[a];
     c->sc.mt_ring = nullptr;
     c->sc.mt_ring_stride = 0;
     c->sc.nemit = static_cast<int32_t>(L.emitters.size());
@@ -432,6 +437,32 @@ static int ensure_lv(bdpt_ctx* c, int rr_depth, uint32_t nslots) {
     return BDPT_OK;
 }
 
+// Interior boxes of the triangle traversal tree are padded by kTriBoxPad x the
+// scene diagonal (wide_bvh.hpp), so a ray that hits a triangle passes through
+// every box above it over a t-interval of at least 2 pad; slab_fast's rounding
+// (RN(1/d), three roundings per plane: < 3.6e-7 (|tn| + |tf|)) can only close
+// that interval for boxes more than ~280 diagonals away along the ray. Every
+// query of a BDPT frame starts inside the scene box or at the camera, so when
+// the camera is within 100 diagonals of the scene the plain tn <= tf test is
+// conservative and the ambiguity slack is skipped. Other rays
+// (bdpt_intersect's, the refleaf tree's unpadded boxes) keep it.
+static uint32_t node_slack_needed(const bdpt_ctx* c, const float* const* origins, int n) {
+    if (!c->tri_tree) return 1u;
+    double diag2 = 0.0;
+    for (int a = 0; a < 3; a++) diag2 += (c->box_hi[a] - c->box_lo[a]) * (c->box_hi[a] - c->box_lo[a]);
+    if (!(diag2 > 0.0) || !std::isfinite(diag2)) return 1u;
+    for (int k = 0; k < n; k++) {
+        double far2 = 0.0;  // squared distance to the farthest corner of the scene box
+        for (int a = 0; a < 3; a++) {
+            const double o = origins[k][a];
+            const double d = std::max(std::fabs(o - c->box_lo[a]), std::fabs(o - c->box_hi[a]));
+            far2 += d * d;
+        }
+        if (!std::isfinite(far2) || far2 > 1.0e4 * diag2) return 1u;
+    }
+    return 0u;
+}
+
 int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_stream) {
     if (!c || !fb) return fail(BDPT_ERR_INVALID, "null argument");
     int rc = check_params(p);
@@ -440,11 +471,13 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const dev::DevFrame fr = make_frame(p);
     const bool hbm = c->sc.lds_bsdf_off == dev::kNoLds;
+    const float* eye[1] = {p->camera.eye};
     if (hbm && p->rr_depth > kLazyRrDepth)
         return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 with BSDF records in HBM (too many materials for the LDS "
                                           "table) is not built");
     if ((rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
     dev::DevScene sc = c->sc;
+    sc.node_slack = node_slack_needed(c, eye, 1);
     if (p->rr_depth > kLazyRrDepth) {  // draws past 226: the lanes' MT19937 rings
         if (!c->mt_ring) HIP_TRY(hipMalloc(&c->mt_ring, sizeof(uint32_t) * 624 * static_cast<size_t>(c->nslots)));
         sc.mt_ring = c->mt_ring;
@@ -824,6 +857,8 @@ static int render_bdpt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const flo
     const dev::DevFrame fr = make_frame(p);
     dev::DevScene sc = c->sc;
     sc.mt_ring = c->mt_state;  // the sample kernel's generator state (mt_state_u32)
+    const float* origins[2] = {p->camera.eye, ray};  // camera connections start at the eye, the walk at ray.o
+    sc.node_slack = node_slack_needed(c, origins, 2);
     const dev::Ray r{dev::f3{ray[0], ray[1], ray[2]}, dev::f3{ray[3], ray[4], ray[5]}, ray[6], ray[7]};
     const uint32_t hdr[4] = {0u, static_cast<uint32_t>(c->splat_cap), 0u, 0u};
     HIP_TRY(hipMemcpyAsync(c->mt_state, state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyHostToDevice,

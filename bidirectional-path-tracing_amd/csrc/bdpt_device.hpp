@@ -50,6 +50,10 @@ struct DevScene {
     const float* __restrict__ emit_cdf;
     const int32_t* __restrict__ shape_emitter;
     uint32_t root_link, wroot_link;
+    // 1: the interior boxes of the traversal tree are tested with slab_fast's
+    // ambiguity slack; 0 (host decision per render, node_slack_needed in
+    // bdpt_capi.cpp): the padded boxes make a plain tn <= tf conservative
+    uint32_t node_slack;
     int32_t nemit, nbsdf, nshapes;
     // LDS copy of the small tables (scene_tables_to_lds): word offsets of the
     // emitter records and the shape->emitter map, total words (16-byte rounded)
@@ -762,6 +766,7 @@ struct TravScene {
     const float4* __restrict__ lbox;
     const float4* __restrict__ wnodes;
     uint32_t wroot_link;
+    uint32_t node_slack;  // 0: interior boxes tested without the ambiguity slack (DevScene::node_slack)
 };
 __device__ __forceinline__ const float4* uniform_ptr(const float4* p) {
     const uint64_t v = reinterpret_cast<uint64_t>(p);
@@ -771,7 +776,8 @@ __device__ __forceinline__ const float4* uniform_ptr(const float4* p) {
 }
 __device__ __forceinline__ TravScene trav_scene(const DevScene& sc) {
     return TravScene{uniform_ptr(sc.wtri), uniform_ptr(sc.lbox), uniform_ptr(sc.wnodes),
-                     static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sc.wroot_link)))};
+                     static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sc.wroot_link))),
+                     static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sc.node_slack)))};
 }
 
 // Triangle tests of one traversal leaf (wtri records). A hit is a candidate of
@@ -845,7 +851,7 @@ __device__ __forceinline__ bool trav_pop(const Ray& r, bool any, TravState& ts, 
 // Interior 4-wide node ts.link: tests the four children, descends into the
 // nearest hit child (true) and stacks the others far-to-near; false when no
 // child is hit (the caller pops).
-template <bool COUNT>
+template <bool COUNT, bool SLACK>
 __device__ __forceinline__ bool trav_node(const TravScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
                                           const Stack& stk, Counts& cnt) {
     if (COUNT) cnt.c[2]++;
@@ -862,7 +868,8 @@ __device__ __forceinline__ bool trav_node(const TravScene& sc, const Ray& r, con
         const uint32_t l = __float_as_uint((&lk.x)[c]);
         float tn, tf;
         const int d = slab_fast(clx, cly, clz, chx, chy, chz, r.o, ri.inv, tn, tf);
-        const bool hit = l != kEmptyLinkDev && d != kSlabMiss && !(tn > far) && !(tf < kCullNear);
+        const bool pass = SLACK ? d != kSlabMiss : !(tn > tf);
+        const bool hit = l != kEmptyLinkDev && pass && !(tn > far) && !(tf < kCullNear);
         key[c] = hit ? tn : __builtin_inff();
         lnk[c] = hit ? l : kEmptyLinkDev;
     }
@@ -901,7 +908,8 @@ __device__ __forceinline__ bool trav_step(const TravScene& sc, const Ray& r, con
     if (ts.link & kLeafBit) {
         if (wleaf_tests<COUNT>(sc.wtri, sc.lbox, ts.link, r, ri, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt))
             return true;
-    } else if (trav_node<COUNT>(sc, r, ri, any, ts, stk, cnt)) {
+    } else if (sc.node_slack ? trav_node<COUNT, true>(sc, r, ri, any, ts, stk, cnt)
+                              : trav_node<COUNT, false>(sc, r, ri, any, ts, stk, cnt)) {
         return false;
     }
     return !trav_pop(r, any, ts, stk, COUNT ? &cnt.c[19] : nullptr);
@@ -920,7 +928,7 @@ __device__ __forceinline__ void trav_while_while(const TravScene& sc, const Ray&
                 cnt.c[8]++;
                 if (first_active_lane()) cnt.c[9]++;
             }
-            if (!trav_node<COUNT>(sc, r, ri, any, ts, stk, cnt) && !trav_pop(r, any, ts, stk)) {
+            if (!trav_node<COUNT, true>(sc, r, ri, any, ts, stk, cnt) && !trav_pop(r, any, ts, stk)) {
                 live = false;
                 break;
             }
