@@ -898,7 +898,7 @@ __device__ __forceinline__ bool trav_node(const TravScene& sc, const Ray& r, con
 
 // One loop iteration (a 4-wide node or a leaf, then the pop). Returns true
 // when the query is complete (result in ts.best / best_t / best_u / best_v).
-template <bool COUNT>
+template <bool COUNT, bool SLACK = true>
 __device__ __forceinline__ bool trav_step(const TravScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
                                           const Stack& stk, Counts& cnt) {
     if (COUNT) {
@@ -908,8 +908,7 @@ __device__ __forceinline__ bool trav_step(const TravScene& sc, const Ray& r, con
     if (ts.link & kLeafBit) {
         if (wleaf_tests<COUNT>(sc.wtri, sc.lbox, ts.link, r, ri, any, ts.best_t, ts.best, ts.best_u, ts.best_v, cnt))
             return true;
-    } else if (sc.node_slack ? trav_node<COUNT, true>(sc, r, ri, any, ts, stk, cnt)
-                              : trav_node<COUNT, false>(sc, r, ri, any, ts, stk, cnt)) {
+    } else if (trav_node<COUNT, SLACK>(sc, r, ri, any, ts, stk, cnt)) {
         return false;
     }
     return !trav_pop(r, any, ts, stk, COUNT ? &cnt.c[19] : nullptr);
@@ -960,7 +959,12 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool a
 #if BDPT_TRAV_WHILE_WHILE
     trav_while_while<COUNT>(tsc, r, ri, any, ts, stk, cnt);
 #else
-    while (!trav_step<COUNT>(tsc, r, ri, any, ts, stk, cnt)) {
+    if (tsc.node_slack) {  // a query-level (uniform) choice: the node step itself has no branch on it
+        while (!trav_step<COUNT, true>(tsc, r, ri, any, ts, stk, cnt)) {
+        }
+    } else {
+        while (!trav_step<COUNT, false>(tsc, r, ri, any, ts, stk, cnt)) {
+        }
     }
 #endif
     bt = ts.best_t, bu = ts.best_u, bv = ts.best_v;

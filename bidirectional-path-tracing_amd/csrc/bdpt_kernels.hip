@@ -85,7 +85,10 @@ struct KParams {
     unsigned long long* counters;
 };
 
-template <bool FULL, bool COUNT>
+// SLACK: interior boxes with slab_fast's ambiguity slack (DevScene::node_slack,
+// decided per render on the host); a template parameter so the node step of
+// the walk loop carries no branch on it.
+template <bool FULL, bool COUNT, bool SLACK>
 __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(const KParams* __restrict__ kpp) {
     const KParams& kp = *kpp;
     __shared__ uint2 stack_mem[kLdsStack * kBlock];
@@ -216,9 +219,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const bool at_leaf = (ts.link & kLeafBit) != 0;
             const uint64_t lv = __ballot(tracing && at_leaf);
             const bool do_leaf = __popcll(lv) * 4 >= __popcll(tr & ~lv) * BDPT_TRAV_SPLIT;
-            if (tracing && at_leaf == do_leaf && trav_step<COUNT>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
+            if (tracing && at_leaf == do_leaf && trav_step<COUNT, SLACK>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
 #else
-            if (tracing && trav_step<COUNT>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
+            if (tracing && trav_step<COUNT, SLACK>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
 #endif
                 res = ts.best, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;
                 tracing = false;
@@ -293,17 +296,20 @@ size_t frame_params_bytes() { return sizeof(dev::KParams); }
 hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
                         uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
                         hipStream_t stream, void* dparams) {
-    const bool full = (fr.flags & 2u) != 0, count = (fr.flags & 1u) != 0;
+    const bool full = (fr.flags & 2u) != 0, count = (fr.flags & 1u) != 0, slack = sc.node_slack != 0;
     const dev::KParams host{sc, fr, fb, lvbuf, gstack, nslots, work, counters};
     hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);
     if (e != hipSuccess) return e;
     const dev::KParams* kp = static_cast<const dev::KParams*>(dparams);
     const dim3 g(grid), b(dev::kBlock);
     const size_t lds = 4 * static_cast<size_t>(sc.lds_words);
-    if (full && count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, true>), g, b, lds, stream, kp);
-    else if (full) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, false>), g, b, lds, stream, kp);
-    else if (count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, true>), g, b, lds, stream, kp);
-    else hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, false>), g, b, lds, stream, kp);
+    // FULL walks the reference's binary tree: SLACK does not apply
+    if (full && count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, true, true>), g, b, lds, stream, kp);
+    else if (full) hipLaunchKernelGGL((dev::bdpt_frame_kernel<true, false, true>), g, b, lds, stream, kp);
+    else if (count && slack) hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, true, true>), g, b, lds, stream, kp);
+    else if (count) hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, true, false>), g, b, lds, stream, kp);
+    else if (slack) hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, false, true>), g, b, lds, stream, kp);
+    else hipLaunchKernelGGL((dev::bdpt_frame_kernel<false, false, false>), g, b, lds, stream, kp);
     return hipGetLastError();
 }
 
@@ -323,7 +329,8 @@ hipError_t launch_sample(const dev::DevScene& sc, const dev::DevFrame& fr, float
 // Resident 256-lane blocks per CU for the frame kernel (VGPR and LDS limited).
 int frame_kernel_blocks_per_cu(size_t dyn_lds) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::bdpt_frame_kernel<false, false>, dev::kBlock, dyn_lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::bdpt_frame_kernel<false, false, false>, dev::kBlock,
+                                                     dyn_lds) !=
             hipSuccess ||
         n <= 0)
         n = BDPT_WAVES_PER_EU;

@@ -14,7 +14,7 @@ python3 - "$f" "$N" <<'PY'
 import csv, sys
 tot = {}
 for r in csv.DictReader(open(sys.argv[1])):
-    if 'bdpt_frame_kernel<false, false>' in r['Kernel_Name']:
+    if 'bdpt_frame_kernel<false, false, false>' in r['Kernel_Name']:
         tot[r['Dispatch_Id']] = tot.get(r['Dispatch_Id'], 0) + float(r['Counter_Value'])
 print(sys.argv[2], 'WRITE_SIZE GB per launch:', [round(v * 1024 / 1e9, 2) for v in tot.values()])
 PY

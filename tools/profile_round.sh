@@ -15,7 +15,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 B="python3 $R/bench.py --no-cpu --scene $SCENE --width $W --height $H --spp $SPP"
-K="bdpt_frame_kernel<false, false>"
+K="bdpt_frame_kernel<false, false, false>"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $B --steps 2 --warmup 1 > $OUT/kt.log 2>&1
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- $B --steps 1 --warmup 0 > $OUT/fetch.log 2>&1
