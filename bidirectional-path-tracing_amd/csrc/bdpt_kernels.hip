@@ -46,6 +46,9 @@ constexpr int kBlock = 256;
 #ifndef BDPT_SEED_CHUNK
 #define BDPT_SEED_CHUNK 1  // refill from per-wave chunks of 64 samples seeded together (0: per-refill seeding)
 #endif
+#ifndef BDPT_WALK_UNROLL
+#define BDPT_WALK_UNROLL 1  // extra interior-node steps per walk iteration (measured: 0: 201.7, 1: 203.6)
+#endif
 #ifndef BDPT_SHADE_READY
 #define BDPT_SHADE_READY 48  // lanes with a finished query that trigger the wave's shading step
 #endif
@@ -219,7 +222,13 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const bool at_leaf = (ts.link & kLeafBit) != 0;
             const uint64_t lv = __ballot(tracing && at_leaf);
             const bool do_leaf = __popcll(lv) * 4 >= __popcll(tr & ~lv) * BDPT_TRAV_SPLIT;
-            if (tracing && at_leaf == do_leaf && trav_step<COUNT, SLACK>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
+            bool fin = tracing && at_leaf == do_leaf && trav_step<COUNT, SLACK>(tsc, L.ray, ri, q_any, ts, stk, cnt);
+            // BDPT_WALK_UNROLL more interior-node steps before the wave's ballots
+#pragma unroll
+            for (int k = 0; k < BDPT_WALK_UNROLL; k++)
+                if (!do_leaf && tracing && !fin && !(ts.link & kLeafBit))
+                    fin = trav_step<COUNT, SLACK>(tsc, L.ray, ri, q_any, ts, stk, cnt);
+            if (fin) {
 #else
             if (tracing && trav_step<COUNT, SLACK>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
 #endif
