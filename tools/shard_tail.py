@@ -1,0 +1,45 @@
+"""Kernel time of one rank's row shard (row_stride N) against the full frame on
+one GPU: the strong-scaling tail a persistent grid pays when each of N ranks
+renders 1/N of the frame (lanes idle once the shard's work counter runs out).
+
+    python tools/shard_tail.py [scene W H spp] [N...]
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in ("bidirectional-path-tracing_amd", "scenes"):
+    sys.path.insert(0, os.path.join(REPO, p))
+import torch  # noqa: E402
+
+import bdpt_amd  # noqa: E402
+import variants  # noqa: E402
+
+
+def main():
+    a = sys.argv[1:]
+    scene, W, H, spp = (a[0], int(a[1]), int(a[2]), int(a[3])) if len(a) >= 4 else ("caustic", 512, 512, 256)
+    ns = [int(x) for x in a[4:]] or [1, 2, 4, 8]
+    sc = variants.SCENES[scene]
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**sc["camera"]), width=W, height=H, spp=spp,
+                          rr_depth=sc["rr_depth"])
+    integ = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(scene)), cfg, device=0)
+    fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda:0")
+    stream = torch.cuda.current_stream().cuda_stream
+    full = None
+    for n in ns:
+        ms = []
+        for rep in range(3):
+            fb.zero_()
+            integ.render_device(fb.data_ptr(), stream, row_offset=0, row_stride=n)
+            ms.append(integ.stats()["kernel_ms"])
+        t = min(ms[1:])
+        if n == 1:
+            full = t
+        ideal = full / n if full else float("nan")
+        print(f"row_stride {n}: kernel {t:.2f} ms, full/{n} = {ideal:.2f} ms, efficiency {ideal / t:.3f}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
