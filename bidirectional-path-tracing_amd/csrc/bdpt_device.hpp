@@ -562,7 +562,7 @@ __device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_
 // conflict-free), deeper ones spill to a per-lane HBM column (rare; the host
 // sizes it to the scene's worst case).
 #ifndef BDPT_LDS_STACK
-#define BDPT_LDS_STACK 8  // traversal-stack entries per lane in LDS (deeper ones spill to HBM, rare)
+#define BDPT_LDS_STACK 7  // traversal-stack entries per lane in LDS (deeper ones spill to HBM, rare); 7 leaves the LDS room for the root nodes
 #endif
 constexpr int kLdsStack = BDPT_LDS_STACK;
 constexpr uint32_t kEmptyLinkDev = 0xffffffffu;  // unused 4-wide child slot
@@ -852,12 +852,21 @@ __device__ __forceinline__ bool trav_pop(const Ray& r, bool any, TravState& ts, 
 // nearest hit child (true) and stacks the others far-to-near; false when no
 // child is hit (the caller pops).
 template <bool COUNT, bool SLACK>
+__device__ __forceinline__ bool trav_node_vals(float4 lx, float4 hx, float4 ly, float4 hy, float4 lz, float4 hz,
+                                               float4 lk, const Ray& r, const RayInv& ri, bool any, TravState& ts,
+                                               const Stack& stk, Counts& cnt);
+template <bool COUNT, bool SLACK>
 __device__ __forceinline__ bool trav_node(const TravScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
                                           const Stack& stk, Counts& cnt) {
-    if (COUNT) cnt.c[2]++;
     const float4* nd = sc.wnodes + 8 * static_cast<size_t>(ts.link);
-    const float4 lx = gld4(nd), hx = gld4(nd + 1), ly = gld4(nd + 2), hy = gld4(nd + 3), lz = gld4(nd + 4),
-                 hz = gld4(nd + 5), lk = gld4(nd + 6);
+    return trav_node_vals<COUNT, SLACK>(gld4(nd), gld4(nd + 1), gld4(nd + 2), gld4(nd + 3), gld4(nd + 4),
+                                        gld4(nd + 5), gld4(nd + 6), r, ri, any, ts, stk, cnt);
+}
+template <bool COUNT, bool SLACK>
+__device__ __forceinline__ bool trav_node_vals(float4 lx, float4 hx, float4 ly, float4 hy, float4 lz, float4 hz,
+                                               float4 lk, const Ray& r, const RayInv& ri, bool any, TravState& ts,
+                                               const Stack& stk, Counts& cnt) {
+    if (COUNT) cnt.c[2]++;
     const float far = cull_far(any ? r.max_t : ts.best_t);
     float key[4];
     uint32_t lnk[4];
