@@ -905,6 +905,51 @@ __device__ __forceinline__ bool trav_node_vals(float4 lx, float4 hx, float4 ly, 
     return true;
 }
 
+// The traversal tree's root node and its interior children (slot k = the
+// root's child k) in LDS, copied by each block at kernel start (before the
+// barrier of scene_tables_to_lds). Every walk starts at the root, so a query's
+// first two node tests run when the lane issues it — with the other lanes of
+// the shading step, from broadcast LDS reads — instead of as the first two
+// global-memory steps of the walk loop (walk_begin_lds).
+struct RootLds {
+    float4 root[7];
+    float4 kid[4 * 7];
+};
+__device__ __forceinline__ bool root_lds_usable(const DevScene& sc) { return !(sc.wroot_link & kLeafBit); }
+__device__ __forceinline__ void root_lds_fill(RootLds& m, const DevScene& sc) {
+    if (!root_lds_usable(sc)) return;
+    const float4* rn = sc.wnodes + 8 * static_cast<size_t>(sc.wroot_link);
+    if (threadIdx.x < 7) {
+        m.root[threadIdx.x] = gld4(rn + threadIdx.x);
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + 28) {
+        const int k = (threadIdx.x - 64) / 7, j = (threadIdx.x - 64) % 7;
+        const float4 lk = gld4(rn + 6);
+        const uint32_t l = __float_as_uint((&lk.x)[k]);
+        if (l != kEmptyLinkDev && !(l & kLeafBit)) m.kid[7 * k + j] = gld4(sc.wnodes + 8 * static_cast<size_t>(l) + j);
+    }
+}
+// The root and (when the walk descends into an interior child) that child;
+// false when the query is already complete (a miss: nothing below was hit).
+template <bool COUNT, bool SLACK>
+__device__ __forceinline__ bool walk_begin_lds(const RootLds& m, const Ray& r, const RayInv& ri, bool any,
+                                               TravState& ts, const Stack& stk, Counts& cnt) {
+    if (COUNT) cnt.c[8]++;
+    bool live = trav_node_vals<COUNT, SLACK>(m.root[0], m.root[1], m.root[2], m.root[3], m.root[4], m.root[5],
+                                             m.root[6], r, ri, any, ts, stk, cnt);
+    if (live && !(ts.link & kLeafBit)) {
+        const float4 lk = m.root[6];
+        const int k = ts.link == __float_as_uint(lk.x) ? 0
+                      : ts.link == __float_as_uint(lk.y) ? 1
+                      : ts.link == __float_as_uint(lk.z) ? 2 : 3;
+        const float4* kn = m.kid + 7 * k;
+        if (COUNT) cnt.c[8]++;
+        live = trav_node_vals<COUNT, SLACK>(kn[0], kn[1], kn[2], kn[3], kn[4], kn[5], kn[6], r, ri, any, ts, stk,
+                                            cnt) ||
+               trav_pop(r, any, ts, stk);
+    }
+    return live;
+}
+
 // One loop iteration (a 4-wide node or a leaf, then the pop). Returns true
 // when the query is complete (result in ts.best / best_t / best_u / best_v).
 template <bool COUNT, bool SLACK = true>

@@ -53,7 +53,7 @@ constexpr int kBlock = 256;
 #define BDPT_SHADE_READY 48  // lanes with a finished query that trigger the wave's shading step
 #endif
 #ifndef BDPT_ROOT_LDS
-#define BDPT_ROOT_LDS 2  // 1: the traversal root node in LDS, tested when a walk begins; 2: and its interior children (measured +1.6 %)
+#define BDPT_ROOT_LDS 1  // 1: the traversal root and its interior children in LDS, tested when a walk begins (RootLds; measured +1.6 %)
 #endif
 
 // One query for the lane's pending state, then the state advance.
@@ -99,21 +99,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     const KParams& kp = *kpp;
     __shared__ uint2 stack_mem[kLdsStack * kBlock];
 #if BDPT_ROOT_LDS && BDPT_OVERLAP
-    // The traversal tree's root node (every walk starts there) in LDS: its test
-    // runs when the walk begins, from a broadcast LDS read.
-    __shared__ float4 root_mem[7];
-    const bool root_in_lds = !FULL && !(kp.sc.wroot_link & kLeafBit);
-    if (root_in_lds && threadIdx.x < 7) root_mem[threadIdx.x] = gld4(kp.sc.wnodes + 8 * kp.sc.wroot_link + threadIdx.x);
-#if BDPT_ROOT_LDS == 2
-    // and its interior children (slot k = the root's child k)
-    __shared__ float4 kid_mem[4 * 7];
-    if (root_in_lds && threadIdx.x >= 64 && threadIdx.x < 64 + 28) {
-        const int k = (threadIdx.x - 64) / 7, j = (threadIdx.x - 64) % 7;
-        const float4 lk = gld4(kp.sc.wnodes + 8 * kp.sc.wroot_link + 6);
-        const uint32_t l = __float_as_uint((&lk.x)[k]);
-        if (l != kEmptyLinkDev && !(l & kLeafBit)) kid_mem[7 * k + j] = gld4(kp.sc.wnodes + 8 * static_cast<size_t>(l) + j);
-    }
-#endif
+    __shared__ RootLds root_lds;
+    const bool root_in_lds = !FULL && root_lds_usable(kp.sc);
+    if (!FULL) root_lds_fill(root_lds, kp.sc);
 #endif
     scene_tables_to_lds(kp.sc);
     const int lane = threadIdx.x & 63;
@@ -228,29 +216,10 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 ts = trav_begin(tsc, L.ray);
                 tracing = true;
 #if BDPT_ROOT_LDS
-                if (root_in_lds) {
-                    if (COUNT) cnt.c[8]++;
-                    bool live = trav_node_vals<COUNT, SLACK>(root_mem[0], root_mem[1], root_mem[2], root_mem[3],
-                                                             root_mem[4], root_mem[5], root_mem[6], L.ray, ri, q_any,
-                                                             ts, stk, cnt);
-#if BDPT_ROOT_LDS == 2
-                    if (live && !(ts.link & kLeafBit)) {  // the nearest child: also an LDS node
-                        const float4 lk = root_mem[6];
-                        const int k = ts.link == __float_as_uint(lk.x) ? 0
-                                      : ts.link == __float_as_uint(lk.y) ? 1
-                                      : ts.link == __float_as_uint(lk.z) ? 2 : 3;
-                        const float4* kn = kid_mem + 7 * k;
-                        if (COUNT) cnt.c[8]++;
-                        live = trav_node_vals<COUNT, SLACK>(kn[0], kn[1], kn[2], kn[3], kn[4], kn[5], kn[6], L.ray,
-                                                            ri, q_any, ts, stk, cnt) ||
-                               trav_pop(L.ray, q_any, ts, stk);
-                    }
-#endif
-                    if (!live) {
-                        res = -1, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;  // no child hit: a miss
-                        tracing = false;
-                        has_res = true;
-                    }
+                if (root_in_lds && !walk_begin_lds<COUNT, SLACK>(root_lds, L.ray, ri, q_any, ts, stk, cnt)) {
+                    res = -1, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;  // no child hit: a miss
+                    tracing = false;
+                    has_res = true;
                 }
 #endif
             }

@@ -233,6 +233,9 @@ enum : int {  // explicit-level steps between queries
 #ifndef PT_TRAV_SPLIT
 #define PT_TRAV_SPLIT 8
 #endif
+#ifndef PT_ROOT_LDS
+#define PT_ROOT_LDS 1  // the overlapped schedule's walks start two levels down (RootLds, as the BDPT megakernel)
+#endif
 #ifndef PT_WAVES_PER_EU
 #define PT_WAVES_PER_EU 4  // 128 VGPRs, 4 blocks of 256 lanes per CU
 #endif
@@ -614,6 +617,11 @@ template <bool COUNT, bool OVERLAP>
 __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const PtParams* __restrict__ pp) {
     const PtParams& P = *pp;
     __shared__ uint2 stack_mem[kLdsStack * 256];
+#if PT_ROOT_LDS
+    __shared__ RootLds root_lds;  // the walk's first two node tests at query issue (bdpt_device.hpp)
+    const bool root_in_lds = OVERLAP && root_lds_usable(P.sc);
+    if (OVERLAP) root_lds_fill(root_lds, P.sc);
+#endif
     scene_tables_to_lds(P.sc);
     const uint32_t slot = blockIdx.x * 256 + threadIdx.x;
     const Stack stk{stack_mem + threadIdx.x, 256, kLdsStack, P.gstack, P.nslots, slot};
@@ -678,6 +686,13 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
             } else {
                 ts = trav_begin(tsc, L.ray);
                 tracing = true;
+#if PT_ROOT_LDS
+                if (root_in_lds && !walk_begin_lds<COUNT, true>(root_lds, L.ray, ri, false, ts, stk, cnt)) {
+                    res = -1, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;  // no child hit: a miss
+                    tracing = false;
+                    has_res = true;
+                }
+#endif
             }
         }
         for (;;) {
