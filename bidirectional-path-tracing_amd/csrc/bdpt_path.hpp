@@ -81,6 +81,10 @@ __device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
     return x;
 }
 
+#ifndef BDPT_CONN_EARLY_COS
+#define BDPT_CONN_EARLY_COS 2  // 1: connectVertices rejects on the cosines before building frames; 2: also connectToLight (+1.3 %); 3: also connectToCamera
+#endif
+
 // ContinuePathRandomWalk (bdpt.h:243-291): BSDF sample (2 draws), throughput,
 // vc / vcm recursion (Georgiev VCM Eqs. 52-54) and the next ray.
 __device__ __forceinline__ bool continue_walk(const BsdfRecord& b, const Hit& h, LazyMT& rng, f3& tp, int& depth,
@@ -398,10 +402,17 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         f3 dir = L.h.p - e_p;
         const float d2 = dot(dir, dir);
         dir = dir * rcp_cr(sqrt_cr(d2));
+#if BDPT_CONN_EARLY_COS >= 2
+        const float cosAtLight = dot(e_n, dir);
+        const float cosAtEye = dot(-dir, L.h.n);  // = the frame's z component (to_local)
+        if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
+        const f3 wi = local_at(L.h.n, -dir);
+#else
         const f3 wi = local_at(L.h.n, -dir);
         const float cosAtLight = dot(e_n, dir);
         const float cosAtEye = wi.z;
         if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
+#endif
         const float pdf_w = div_cr((e_pdf * e_pos_pdf) * d2, cosAtLight);
         const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
         const f3 Li = ((ep.f * rcp_cr(pdf_w)) * L.c.tp) * ld3(e.radiance);
@@ -433,10 +444,18 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         if (xp < 0 || yp < 0 || xp >= fr.W || yp >= fr.H) break;
         const float cosCamera = dot(fwd, e2l);
         if (cosCamera <= 0.f) break;
+#if BDPT_CONN_EARLY_COS >= 3
+        if (dot(-e2l, L.h.n) <= 0.f) break;  // wi.z <= 0 (the frame z component, to_local)
+        const f3 wi = local_at(L.h.n, -e2l);
+        const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
+        const f3 f = ep.f;
+        if (is_zero(f)) break;
+#else
         const f3 wi = local_at(L.h.n, -e2l);
         const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
         const f3 f = ep.f;
         if (is_zero(f) || wi.z <= 0.f) break;
+#endif
         const float d = div_cr(fr.cam.vnear, cosCamera);
         const float img2solid = div_cr(d * d, cosCamera);
         const float img2surf = img2solid * (wi.z * invD2);
@@ -466,6 +485,17 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             f3 dir = L.h.p - V.p;
             const float invD2 = rcp_cr(dot(dir, dir));
             dir = dir * sqrt_cr(invD2);
+#if BDPT_CONN_EARLY_COS >= 1
+            // the frames' z components are dot(v, n) (to_local), so the
+            // rejection test runs before the frames are built
+            const float cosL = dot(dir, V.n), cosE = dot(-dir, L.h.n);
+            if (cosL <= 0.f || cosE <= 0.f) {
+                L.c.ci++;
+                continue;
+            }
+            const f3 wiL = local_at(V.n, dir);  // Frame(n) is a pure function of n
+            const f3 wiE = local_at(L.h.n, -dir);
+#else
             const f3 wiL = local_at(V.n, dir);  // Frame(n) is a pure function of n
             const f3 wiE = local_at(L.h.n, -dir);
             const float cosL = wiL.z, cosE = wiE.z;
@@ -473,6 +503,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 L.c.ci++;
                 continue;
             }
+#endif
             const BsdfRecord& bl = bsdf_of(sc, V.mat);
             const EvalPdfs eL = bsdf_eval_pdfs(bl, wiL, V.wo), eE = bsdf_eval_pdfs(be, wiE, L.h.wo);
             f3 Li = eL.f * eE.f;
