@@ -82,7 +82,7 @@ __device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
 }
 
 #ifndef BDPT_CONN_EARLY_COS
-#define BDPT_CONN_EARLY_COS 2  // 1: connectVertices rejects on the cosines before building frames; 2: also connectToLight (+1.3 %); 3: also connectToCamera
+#define BDPT_CONN_EARLY_COS 3  // 1: connectVertices rejects on the cosines before building frames; 2: also connectToLight (+1.3 %); 3: also connectToCamera (+0.6 %)
 #endif
 
 // ContinuePathRandomWalk (bdpt.h:243-291): BSDF sample (2 draws), throughput,
