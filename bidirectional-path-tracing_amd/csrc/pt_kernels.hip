@@ -233,6 +233,9 @@ enum : int {  // explicit-level steps between queries
 #ifndef PT_TRAV_SPLIT
 #define PT_TRAV_SPLIT 8
 #endif
+#ifndef PT_EARLY_COS
+#define PT_EARLY_COS 1  // emitter samples rejected on the cosine (dot(v, n), the frame z) before the shading frame is built (+0.7 % path tracer)
+#endif
 #ifndef PT_ROOT_LDS
 #define PT_ROOT_LDS 1  // the overlapped schedule's walks start two levels down (RootLds, as the BDPT megakernel)
 #endif
@@ -284,11 +287,19 @@ void pt_advance(PtLane& L, int ps, f3 Lr, const PtParams& P, uint32_t slot) {
                 f3 en, ep;
                 const int id = sample_emitter(sc, L.rng, epdf, en, ep, eapdf);
                 const f3 wiW = normalize(ep - L.h.p);
+#if PT_EARLY_COS
+                const f3 dd = L.h.p - ep;  // glm::distance2(positionOut, hit.p)
+                const float d2 = dot(dd, dd);
+                const float cosOut = dot(-wiW, en);
+                if (cosOut > 0.f && dot(wiW, L.h.n) > 0.f) {  // dot(v, n) = the frame's z (to_local)
+                    const f3 wil = local_at(L.h.n, wiW);
+#else
                 const f3 wil = local_at(L.h.n, wiW);
                 const f3 dd = L.h.p - ep;  // glm::distance2(positionOut, hit.p)
                 const float d2 = dot(dd, dd);
                 const float cosOut = dot(-wiW, en);
                 if (cosOut > 0.f && wil.z > 0.f) {
+#endif
                     L.e_shape = emitter_of(sc, id).shape;
                     L.e_cos = cosOut, L.e_d2 = d2, L.e_pdf = epdf, L.e_apdf = eapdf, L.e_wil = wil;
                     L.ray = pt_ray(L.h.p, wiW);
@@ -405,8 +416,13 @@ void pt_advance(PtLane& L, int ps, f3 Lr, const PtParams& P, uint32_t slot) {
                     const f3 dd = L.h.p - pos;
                     const float d2 = dot(dd, dd);
                     const float cosOut = dot(-wiW, ne);
+#if PT_EARLY_COS
+                    if (cosOut <= 0.f || dot(wiW, L.h.n) <= 0.f) break;
+                    const f3 wil = local_at(L.h.n, wiW);
+#else
                     const f3 wil = local_at(L.h.n, wiW);
                     if (cosOut <= 0.f || wil.z <= 0.f) break;
+#endif
                     L.e_id = static_cast<int>(id), L.e_pdf = epdf, L.e_apdf = pdf, L.e_wil = wil;
                     L.e_cos = cosOut * rcp_cr(d2);  // areaToSolidAngle
                     L.ray = Ray{L.h.p, wiW, kEpsilon, sqrt_cr(d2) - kEpsilon};
@@ -415,8 +431,13 @@ void pt_advance(PtLane& L, int ps, f3 Lr, const PtParams& P, uint32_t slot) {
                 }
                 float pdf;  // solid angle (direct.h:262-309) or MIS (:333-372)
                 const f3 wiW = sphere_solid_angle(u, L.h.p, center, e.radius, pdf);
+#if PT_EARLY_COS
+                if (dot(wiW, L.h.n) <= 0.f) break;
+                const f3 wil = local_at(L.h.n, wiW);
+#else
                 const f3 wil = local_at(L.h.n, wiW);
                 if (wil.z <= 0.f) break;
+#endif
                 L.e_id = static_cast<int>(id), L.e_pdf = epdf, L.e_apdf = pdf, L.e_wil = wil;
                 const f3 dc = center - L.h.p;
                 L.ray = Ray{L.h.p, wiW, kEpsilon, st == DI_SOLID_ANGLE ? sqrt_cr(dot(dc, dc)) + kEpsilon
