@@ -56,7 +56,8 @@ class _Camera(ctypes.Structure):
 class _FrameParams(ctypes.Structure):
     _fields_ = [("camera", _Camera), ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
                 ("rr_depth", ctypes.c_int32), ("strategy", ctypes.c_int32), ("seed_base", ctypes.c_uint32),
-                ("row_offset", ctypes.c_int32), ("row_stride", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+                ("row_offset", ctypes.c_int32), ("row_stride", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("russian_roulette", ctypes.c_int32)]
 
 
 class _SceneInfo(ctypes.Structure):
@@ -110,6 +111,58 @@ class _MultiStats(ctypes.Structure):  # bdpt_multi_stats
                 ("kernel_ms", ctypes.c_double * MAX_DEVICES), ("device_samples", ctypes.c_int64 * MAX_DEVICES)]
 
 
+class _MaterialDesc(ctypes.Structure):  # bdpt_material_desc
+    _fields_ = [("illum", ctypes.c_int32), ("kd", ctypes.c_float * 3), ("ks", ctypes.c_float * 3),
+                ("ke", ctypes.c_float * 3), ("tf", ctypes.c_float * 3), ("ns", ctypes.c_float), ("ni", ctypes.c_float),
+                ("scale", ctypes.c_float), ("spec_weight", ctypes.c_float), ("has_texture", ctypes.c_int32)]
+
+
+class _EmitterDesc(ctypes.Structure):  # bdpt_emitter_desc
+    _fields_ = [("shape", ctypes.c_int32), ("area", ctypes.c_float), ("radiance", ctypes.c_float * 3),
+                ("ncdf", ctypes.c_int32), ("cdf", ctypes.c_void_p)]
+
+
+class _BvhNodeDesc(ctypes.Structure):  # bdpt_bvh_node_desc
+    _fields_ = [("bmin", ctypes.c_float * 3), ("bmax", ctypes.c_float * 3), ("start", ctypes.c_uint32),
+                ("nprims", ctypes.c_uint32), ("right_offset", ctypes.c_uint32)]
+
+
+class _SceneDesc(ctypes.Structure):  # bdpt_scene_desc
+    _fields_ = [("triangles", ctypes.c_int64), ("positions", ctypes.c_void_p), ("normals", ctypes.c_void_p),
+                ("tri_shape", ctypes.c_void_p), ("tri_prim", ctypes.c_void_p), ("tri_mat", ctypes.c_void_p),
+                ("shapes", ctypes.c_int32), ("materials", ctypes.c_int32), ("material", ctypes.c_void_p),
+                ("emitters", ctypes.c_int32), ("emitter", ctypes.c_void_p), ("bvh_nodes", ctypes.c_int64),
+                ("bvh", ctypes.c_void_p), ("bvh_order", ctypes.c_void_p)]
+
+
+# BsdfKind (bdpt_types.h) -> the MTL illum that selects it (renderer.cpp:258-271)
+KIND_ILLUM = {0: 5, 1: 7, 2: 3, 3: 6, 4: 8, 5: 2}
+LAYOUT_ARRAYS = ("tri", "shade", "nodes", "wnodes", "wtri", "lbox", "bsdfs", "emitters", "emit_tri", "emit_cdf",
+                 "shape_emitter", "roots")  # bdpt_scene_export_layout ids 0..11
+
+
+@dataclass
+class SceneDesc:
+    """bdpt_scene_desc as numpy arrays: the Scene a caller already holds in memory
+    (core.h:352-358) - triangles in (shape, face) order, materials with their
+    constructed constants, emitters with their CDFs, the flat Fast-BVH and the
+    BVH's object order."""
+    positions: np.ndarray   # float32 (n, 9)
+    normals: np.ndarray     # float32 (n, 9)
+    tri_shape: np.ndarray   # int32 (n,)
+    tri_prim: np.ndarray
+    tri_mat: np.ndarray
+    shapes: int
+    materials: list         # dicts: illum kd ks ke tf ns ni scale spec_weight has_texture
+    emitters: list          # dicts: shape area radiance cdf
+    bvh: np.ndarray         # structured (bmin f4[3], bmax f4[3], start u4, nprims u4, right_offset u4)
+    bvh_order: np.ndarray   # int32 (n,)
+
+
+BVH_NODE_DTYPE = np.dtype([("bmin", "<f4", 3), ("bmax", "<f4", 3), ("start", "<u4"), ("nprims", "<u4"),
+                           ("right_offset", "<u4")])
+
+
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
                 ("counters", ctypes.c_int64 * len(COUNTER_NAMES))]  # BDPT_NUM_COUNTERS
@@ -156,6 +209,8 @@ def lib():
         L.bdpt_scene_get_info.argtypes = [vp, ctypes.POINTER(_SceneInfo)]
         L.bdpt_scene_export.argtypes = [vp, vp, vp, vp, vp]
         L.bdpt_scene_export_traversal.argtypes = [vp, vp, vp, vp, vp]
+        L.bdpt_scene_create.argtypes = [ctypes.POINTER(_SceneDesc), ctypes.POINTER(vp)]
+        L.bdpt_scene_export_layout.argtypes = [vp, i32, vp, ctypes.POINTER(ctypes.c_int64)]
         L.bdpt_camera_constants.argtypes = [ctypes.POINTER(_Camera), i32, i32, f32p]
         L.bdpt_device_count.argtypes = [ctypes.POINTER(i32)]
         L.bdpt_ctx_create.argtypes = [vp, i32, ctypes.POINTER(vp)]
@@ -398,6 +453,82 @@ class Scene:
         _check(lib().bdpt_scene_load_obj(obj_path.encode(), ctypes.byref(h)))
         self._h = h
         self.path = obj_path
+
+    @classmethod
+    def from_desc(cls, d: SceneDesc) -> "Scene":
+        """bdpt_scene_create: the scene handed over from arrays the caller holds."""
+        keep = []
+
+        def arr(a, dt, shape=None):
+            a = np.ascontiguousarray(np.asarray(a, dt))
+            if shape is not None:
+                a = a.reshape(shape)
+            keep.append(a)
+            return a.ctypes.data
+
+        n = int(np.asarray(d.tri_shape).size)
+        mats = (_MaterialDesc * max(len(d.materials), 1))()
+        for k, m in enumerate(d.materials):
+            mats[k].illum = int(m["illum"])
+            for f in ("kd", "ks", "ke", "tf"):
+                getattr(mats[k], f)[:] = [float(x) for x in m[f]]
+            mats[k].ns, mats[k].ni = float(m["ns"]), float(m["ni"])
+            mats[k].scale, mats[k].spec_weight = float(m.get("scale", 1.0)), float(m.get("spec_weight", 0.0))
+            mats[k].has_texture = int(m.get("has_texture", 0))
+        ems = (_EmitterDesc * max(len(d.emitters), 1))()
+        for k, e in enumerate(d.emitters):
+            ems[k].shape, ems[k].area = int(e["shape"]), float(e["area"])
+            ems[k].radiance[:] = [float(x) for x in e["radiance"]]
+            ems[k].ncdf = int(np.asarray(e["cdf"]).size)
+            ems[k].cdf = arr(e["cdf"], np.float32)
+        c = _SceneDesc()
+        c.triangles = n
+        c.positions, c.normals = arr(d.positions, np.float32), arr(d.normals, np.float32)
+        c.tri_shape, c.tri_prim, c.tri_mat = arr(d.tri_shape, np.int32), arr(d.tri_prim, np.int32), arr(d.tri_mat,
+                                                                                                           np.int32)
+        c.shapes, c.materials, c.material = int(d.shapes), len(d.materials), ctypes.addressof(mats)
+        c.emitters, c.emitter = len(d.emitters), ctypes.addressof(ems)
+        bvh = np.ascontiguousarray(np.asarray(d.bvh, BVH_NODE_DTYPE))
+        keep.append(bvh)
+        c.bvh_nodes, c.bvh = int(bvh.size), bvh.ctypes.data
+        c.bvh_order = arr(d.bvh_order, np.int32)
+        h = ctypes.c_void_p()
+        _check(lib().bdpt_scene_create(ctypes.byref(c), ctypes.byref(h)))
+        self = cls.__new__(cls)
+        self._h, self.path = h, None
+        return self
+
+    def export_layout(self, array) -> bytes:
+        """bdpt_scene_export_layout: one of the device arrays (LAYOUT_ARRAYS) as bytes."""
+        i = LAYOUT_ARRAYS.index(array) if isinstance(array, str) else int(array)
+        n = ctypes.c_int64(0)
+        _check(lib().bdpt_scene_export_layout(self._h, i, None, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(max(n.value, 1))
+        _check(lib().bdpt_scene_export_layout(self._h, i, buf, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
+    def to_desc(self) -> SceneDesc:
+        """The descriptor of this scene, rebuilt from its exports (BVH leaf order back
+        to (shape, face) order; materials and emitters from the device records)."""
+        inf = self.info()
+        tf, ti, nf, nu = self.export()
+        perm = np.lexsort((ti[:, 1], ti[:, 0]))  # (shape, prim) order
+        order = np.empty_like(perm)
+        order[perm] = np.arange(perm.size)
+        rec = np.frombuffer(self.export_layout("bsdfs"), np.uint32).reshape(-1, 18)
+        recf = rec.view(np.float32)
+        mats = [dict(illum=KIND_ILLUM[int(r[0])], kd=f[2:5], ks=f[5:8], tf=f[8:11], ke=f[11:14], ns=f[14], ni=f[15],
+                     scale=f[16], spec_weight=f[17]) for r, f in zip(rec, recf)]
+        em = np.frombuffer(self.export_layout("emitters"), np.int32).reshape(-1, 12)
+        cdf = np.frombuffer(self.export_layout("emit_cdf"), np.float32)
+        ems = [dict(shape=int(e[0]), area=e.view(np.float32)[4], radiance=e.view(np.float32)[5:8],
+                    cdf=cdf[e[3]:e[3] + e[1] + 1]) for e in em]
+        bvh = np.zeros(nf.shape[0], BVH_NODE_DTYPE)
+        bvh["bmin"], bvh["bmax"] = nf[:, :3], nf[:, 3:]
+        bvh["start"], bvh["nprims"], bvh["right_offset"] = nu[:, 0], nu[:, 1], nu[:, 2]
+        return SceneDesc(positions=tf[perm, :9], normals=tf[perm, 9:], tri_shape=ti[perm, 0], tri_prim=ti[perm, 1],
+                         tri_mat=ti[perm, 2], shapes=inf["shapes"], materials=mats, emitters=ems, bvh=bvh,
+                         bvh_order=order.astype(np.int32))
 
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:

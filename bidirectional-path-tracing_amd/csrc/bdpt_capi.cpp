@@ -178,6 +178,46 @@ int bdpt_scene_load_obj(const char* obj_path, bdpt_scene** out) {
     return BDPT_OK;
 }
 
+int bdpt_scene_create(const bdpt_scene_desc* desc, bdpt_scene** out) {
+    if (!desc || !out) return fail(BDPT_ERR_INVALID, "null argument");
+    auto s = std::make_unique<bdpt_scene>();
+    std::string err;
+    if (!load_desc_scene(*desc, s->host, err)) return fail(BDPT_ERR_INVALID, err);
+    if (!build_device_layout(s->host, s->layout, err)) return fail(BDPT_ERR_INVALID, err);
+    *out = s.release();
+    return BDPT_OK;
+}
+
+int bdpt_scene_export_layout(const bdpt_scene* s, int32_t array, void* dst, int64_t* bytes) {
+    if (!s || !bytes) return fail(BDPT_ERR_INVALID, "null argument");
+    const DeviceLayout& L = s->layout;
+    const uint32_t roots[4] = {L.root_link, L.wroot_link, static_cast<uint32_t>(L.wmax_stack),
+                               static_cast<uint32_t>(L.wdepth)};
+    const void* src = nullptr;
+    size_t n = 0;
+    switch (array) {
+        case 0: src = L.tri.data(), n = L.tri.size() * 16; break;
+        case 1: src = L.shade.data(), n = L.shade.size() * 16; break;
+        case 2: src = L.nodes.data(), n = L.nodes.size() * 16; break;
+        case 3: src = L.wnodes.data(), n = L.wnodes.size() * 16; break;
+        case 4: src = L.wtri.data(), n = L.wtri.size() * 16; break;
+        case 5: src = L.lbox.data(), n = L.lbox.size() * 16; break;
+        case 6: src = L.bsdfs.data(), n = L.bsdfs.size() * sizeof(BsdfRecord); break;
+        case 7: src = L.emitters.data(), n = L.emitters.size() * sizeof(EmitterRecord); break;
+        case 8: src = L.emit_tri.data(), n = L.emit_tri.size() * 16; break;
+        case 9: src = L.emit_cdf.data(), n = L.emit_cdf.size() * 4; break;
+        case 10: src = L.shape_emitter.data(), n = L.shape_emitter.size() * 4; break;
+        case 11: src = roots, n = sizeof(roots); break;
+        default: return fail(BDPT_ERR_INVALID, "unknown layout array");
+    }
+    if (dst) {
+        if (*bytes < static_cast<int64_t>(n)) return fail(BDPT_ERR_INVALID, "destination too small");
+        if (n) std::memcpy(dst, src, n);
+    }
+    *bytes = static_cast<int64_t>(n);
+    return BDPT_OK;
+}
+
 int bdpt_scene_free(bdpt_scene* scene) {
     delete scene;
     return BDPT_OK;
@@ -410,6 +450,7 @@ static int check_params(const bdpt_frame_params* p) {
         return fail(BDPT_ERR_UNSUPPORTED, "unknown flag (bit 2, the round-1 wavefront schedule, was removed)");
     if (p->strategy < 0 || p->strategy > 2) return fail(BDPT_ERR_INVALID, "unknown strategy");
     if (p->row_stride < 1 || p->row_offset < 0) return fail(BDPT_ERR_INVALID, "bad row shard");
+    if (p->russian_roulette != BDPT_RR_NONE) return fail(BDPT_ERR_UNSUPPORTED, "russian_roulette mode not built");
     return BDPT_OK;
 }
 
@@ -852,38 +893,48 @@ static int render_bdpt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const flo
     HIP_TRY(hipSetDevice(c->device));
     if ((rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
     // a sample splats at most once per light vertex: rr_depth bounds the list
+    // without Russian roulette; with it the list grows on demand (below)
     if ((rc = ensure_sample_buffers(c, std::max(p->rr_depth, 1)))) return rc;
-    if ((rc = begin_use(c, c->stream))) return rc;
     const dev::DevFrame fr = make_frame(p);
     dev::DevScene sc = c->sc;
     sc.mt_ring = c->mt_state;  // the sample kernel's generator state (mt_state_u32)
     const float* origins[2] = {p->camera.eye, ray};  // camera connections start at the eye, the walk at ray.o
     sc.node_slack = node_slack_needed(c, origins, 2);
     const dev::Ray r{dev::f3{ray[0], ray[1], ray[2]}, dev::f3{ray[3], ray[4], ray[5]}, ray[6], ray[7]};
-    const uint32_t hdr[4] = {0u, static_cast<uint32_t>(c->splat_cap), 0u, 0u};
-    HIP_TRY(hipMemcpyAsync(c->mt_state, state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyHostToDevice,
-                           c->stream));
-    HIP_TRY(hipMemcpyAsync(c->splat_list, hdr, sizeof(hdr), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(launch_sample(sc, fr, c->splat_list, c->lv, c->gstack, r, c->sample_out, c->stream));
-    std::vector<float> list(4 * (static_cast<size_t>(c->splat_cap) + 1));
+    uint32_t st_out[BDPT_MT19937_WORDS];
+    std::vector<float> list;
     float out[4];
-    HIP_TRY(hipMemcpyAsync(out, c->sample_out, sizeof(out), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(list.data(), c->splat_list, list.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(state, c->mt_state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyDeviceToHost,
-                           c->stream));
-    if ((rc = end_use(c, c->stream))) return rc;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    uint32_t n;
-    std::memcpy(&n, &list[0], 4);
-    if (n > static_cast<uint32_t>(c->splat_cap)) return fail(BDPT_ERR_HIP, "splat list overflow");
+    uint32_t n = 0;
+    for (int attempt = 0;; attempt++) {
+        if ((rc = begin_use(c, c->stream))) return rc;
+        const uint32_t hdr[4] = {0u, static_cast<uint32_t>(c->splat_cap), 0u, 0u};
+        HIP_TRY(hipMemcpyAsync(c->mt_state, state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyHostToDevice,
+                               c->stream));
+        HIP_TRY(hipMemcpyAsync(c->splat_list, hdr, sizeof(hdr), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(launch_sample(sc, fr, c->splat_list, c->lv, c->gstack, r, c->sample_out, c->stream));
+        list.assign(4 * (static_cast<size_t>(c->splat_cap) + 1), 0.f);
+        HIP_TRY(hipMemcpyAsync(out, c->sample_out, sizeof(out), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(list.data(), c->splat_list, list.size() * sizeof(float), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipMemcpyAsync(st_out, c->mt_state, sizeof(st_out), hipMemcpyDeviceToHost, c->stream));
+        if ((rc = end_use(c, c->stream))) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        std::memcpy(&n, &list[0], 4);
+        if (n <= static_cast<uint32_t>(c->splat_cap)) break;
+        // more splats than the device list holds (the kernel counts them all):
+        // grow it and run the sample again from the caller's unchanged state
+        if (attempt > 0) return fail(BDPT_ERR_HIP, "splat list overflow");
+        if ((rc = ensure_sample_buffers(c, static_cast<int32_t>(n)))) return rc;
+    }
     *nsplats = static_cast<int32_t>(n);
-    if (static_cast<int32_t>(n) > capacity)
+    if (static_cast<int32_t>(n) > capacity)  // the caller's state is left as it was
         return fail(BDPT_ERR_INVALID, "splat capacity too small (" + std::to_string(n) + " splats)");
     for (uint32_t k = 0; k < n; k++) {
         const float* e = &list[4 + 4 * static_cast<size_t>(k)];
         std::memcpy(&splats[k].pixel, &e[0], 4);
         splats[k].rgb[0] = e[1], splats[k].rgb[1] = e[2], splats[k].rgb[2] = e[3];
     }
+    std::memcpy(state, st_out, sizeof(st_out));
     Li[0] = out[0], Li[1] = out[1], Li[2] = out[2];
     if (taken) std::memcpy(taken, &out[3], 4);
     return BDPT_OK;
@@ -910,6 +961,10 @@ int bdpt_render_sample(bdpt_ctx* c, const bdpt_frame_params* p, const float ray[
     std::vector<bdpt_splat> sp(static_cast<size_t>(std::max(p->rr_depth, 1)));
     int32_t n = 0;
     int rc = render_bdpt_sample(c, p, ray, st, Li, sp.data(), static_cast<int32_t>(sp.size()), &n, &used);
+    if (rc == BDPT_ERR_INVALID && n > static_cast<int32_t>(sp.size())) {  // Russian roulette: a longer list
+        sp.resize(static_cast<size_t>(n));
+        rc = render_bdpt_sample(c, p, ray, st, Li, sp.data(), n, &n, &used);
+    }
     if (rc) return rc;
     for (int32_t k = 0; k < n; k++) {  // rgb[pixel] += radiance * misWeight, in the sample's order
         float* px = fb_host + 3 * static_cast<size_t>(sp[k].pixel);

@@ -487,6 +487,40 @@ void build_bvh(HostScene& s) {
     }
 }
 
+// The BSDF the reference constructs for a material (renderer.cpp:258-271):
+// kind and EBSDFType bits by illum, the MTL constants; the mixture / Phong
+// constructor constants (scale, specw) are filled by the caller.
+BsdfRecord bsdf_record(const Material& m) {
+    BsdfRecord b{};
+    for (int k = 0; k < 3; k++) {
+        b.kd[k] = m.Kd[k], b.ks[k] = m.Ks[k], b.tf[k] = m.Tf[k], b.emission[k] = m.Ke[k];
+    }
+    b.exponent = m.Ns;
+    b.ior = m.Ni;
+    b.scale = 1.f;
+    switch (m.illum) {
+        case 7: b.kind = BSDF_DIFFUSE, b.type = kTypeDiffuseRefl; break;
+        case 3: b.kind = BSDF_MIRROR, b.type = kTypeDeltaRefl; break;
+        case 6: b.kind = BSDF_GLASS, b.type = kTypeDeltaRefl | kTypeDeltaTrans; break;
+        case 5: b.kind = BSDF_NULL, b.type = 0; break;
+        default: b.kind = (m.illum == 8) ? BSDF_MIXTURE : BSDF_PHONG, b.type = kTypeGlossyRefl | kTypeDiffuseRefl;
+    }
+    return b;
+}
+
+// Scene::load dereferences the BSDF of every shape's first face
+// (renderer.cpp:277-278: bsdf->isEmissive()); a null BSDF there would crash it.
+bool check_shape_bsdfs(const HostScene& s, std::string& err) {
+    for (size_t sh = 0; sh < s.shape_first.size(); sh++) {
+        if (s.shape_count[sh] == 0) continue;
+        if (s.bsdfs[s.tri_mat[s.shape_first[sh]]].kind == BSDF_NULL) {
+            err = "shape " + std::to_string(sh) + " uses a null BSDF (illum 5) on its first face";
+            return false;
+        }
+    }
+    return true;
+}
+
 }  // namespace
 
 bool load_obj_scene(const std::string& obj_path, HostScene& s, std::string& err) {
@@ -538,22 +572,9 @@ bool load_obj_scene(const std::string& obj_path, HostScene& s, std::string& err)
             err = "material '" + m.name + "' uses a bitmap texture (not supported)";
             return false;
         }
-        BsdfRecord b{};
-        for (int k = 0; k < 3; k++) {
-            b.kd[k] = m.Kd[k], b.ks[k] = m.Ks[k], b.tf[k] = m.Tf[k], b.emission[k] = m.Ke[k];
-        }
-        b.exponent = m.Ns;
-        b.ior = m.Ni;
-        b.scale = 1.f;
-        switch (m.illum) {
-            case 7: b.kind = BSDF_DIFFUSE, b.type = kTypeDiffuseRefl; break;
-            case 3: b.kind = BSDF_MIRROR, b.type = kTypeDeltaRefl; break;
-            case 6: b.kind = BSDF_GLASS, b.type = kTypeDeltaRefl | kTypeDeltaTrans; break;
-            case 5: b.kind = BSDF_NULL, b.type = 0; break;
-            default: b.kind = (m.illum == 8) ? BSDF_MIXTURE : BSDF_PHONG, b.type = kTypeGlossyRefl | kTypeDiffuseRefl;
-        }
+        BsdfRecord b = bsdf_record(m);
         if (b.kind == BSDF_MIXTURE || b.kind == BSDF_PHONG) {
-            // mixture.h:39-46: energy-conserving scale and specular sampling weight.
+            // mixture.h:39-46 / phong.h:40-47: energy-conserving scale and specular sampling weight.
             F3 mx = load3(b.ks) + load3(b.kd);
             float actualMax = std::max(std::max(mx.x, mx.y), mx.z);
             b.scale = actualMax > 1.0f ? 0.99f * (1.0f / actualMax) : 1.0f;
@@ -564,13 +585,10 @@ bool load_obj_scene(const std::string& obj_path, HostScene& s, std::string& err)
         }
         s.bsdfs.push_back(b);
     }
+    if (!check_shape_bsdfs(s, err)) return false;
     // Emitters: shapes whose first face's BSDF emits (renderer.cpp:279-305).
     for (int sh = 0; sh < nshapes; sh++) {
         const BsdfRecord& b = s.bsdfs[s.tri_mat[s.shape_first[sh]]];
-        if (b.kind == BSDF_NULL) {
-            err = "shape " + std::to_string(sh) + " uses a null BSDF (illum 5) on its first face";
-            return false;
-        }
         F3 e = load3(b.emission);
         if (!(dot(e, e) > 0.f)) continue;
         Emitter em;
@@ -589,6 +607,171 @@ bool load_obj_scene(const std::string& obj_path, HostScene& s, std::string& err)
         s.emitters.push_back(std::move(em));
     }
     build_bvh(s);
+    return true;
+}
+
+// ------------------------------------------------------ caller's Scene (desc)
+bool load_desc_scene(const bdpt_scene_desc& d, HostScene& s, std::string& err) {
+    s = HostScene();
+    if (d.triangles <= 0 || !d.positions || !d.normals || !d.tri_shape || !d.tri_prim || !d.tri_mat) {
+        err = "scene descriptor: no triangles or a null triangle array";
+        return false;
+    }
+    if (d.shapes <= 0 || d.materials <= 0 || !d.material || d.emitters < 0 || (d.emitters > 0 && !d.emitter) ||
+        d.bvh_nodes <= 0 || !d.bvh || !d.bvh_order) {
+        err = "scene descriptor: bad shape / material / emitter / BVH table";
+        return false;
+    }
+    const size_t n = static_cast<size_t>(d.triangles);
+    if (n >= (1u << 28)) {
+        err = "more than 2^28 triangles";
+        return false;
+    }
+    s.pos.assign(d.positions, d.positions + 9 * n);
+    s.nrm.assign(d.normals, d.normals + 9 * n);
+    s.tri_shape.assign(d.tri_shape, d.tri_shape + n);
+    s.tri_prim.assign(d.tri_prim, d.tri_prim + n);
+    s.tri_mat.assign(d.tri_mat, d.tri_mat + n);
+    // AcceleratorBVH::build (accel.h:115-123) lists the triangles shape by shape,
+    // faces in mesh order: primID = face index within its shape.
+    s.shape_first.assign(d.shapes, 0);
+    s.shape_count.assign(d.shapes, 0);
+    s.shape_emitter.assign(d.shapes, -1);
+    for (size_t i = 0; i < n; i++) {
+        const int32_t sh = s.tri_shape[i];
+        if (sh < 0 || sh >= d.shapes || (i > 0 && sh < s.tri_shape[i - 1])) {
+            err = "scene descriptor: triangle " + std::to_string(i) + " is not in (shape, face) order";
+            return false;
+        }
+        if (s.shape_count[sh] == 0) s.shape_first[sh] = static_cast<int32_t>(i);
+        if (s.tri_prim[i] != s.shape_count[sh]) {
+            err = "scene descriptor: triangle " + std::to_string(i) + " has primID " + std::to_string(s.tri_prim[i]) +
+                  ", expected its face index " + std::to_string(s.shape_count[sh]);
+            return false;
+        }
+        s.shape_count[sh]++;
+        if (s.tri_mat[i] < 0 || s.tri_mat[i] >= d.materials) {
+            err = "scene descriptor: triangle " + std::to_string(i) + " has no valid material";
+            return false;
+        }
+    }
+    for (int32_t m = 0; m < d.materials; m++) {
+        const bdpt_material_desc& md = d.material[m];
+        if (md.has_texture) {
+            err = "material " + std::to_string(m) + " uses a bitmap texture (not supported)";
+            return false;
+        }
+        Material mt;
+        mt.name = "material" + std::to_string(m);
+        mt.illum = md.illum;
+        for (int k = 0; k < 3; k++) mt.Kd[k] = md.kd[k], mt.Ks[k] = md.ks[k], mt.Ke[k] = md.ke[k], mt.Tf[k] = md.tf[k];
+        mt.Ns = md.ns;
+        mt.Ni = md.ni;
+        s.materials.push_back(mt);
+        BsdfRecord b = bsdf_record(mt);
+        if (b.kind == BSDF_MIXTURE || b.kind == BSDF_PHONG) {  // the caller's constructed values
+            b.scale = md.scale;
+            b.specw = md.spec_weight;
+        }
+        s.bsdfs.push_back(b);
+    }
+    if (!check_shape_bsdfs(s, err)) return false;
+    for (int32_t k = 0; k < d.emitters; k++) {
+        const bdpt_emitter_desc& ed = d.emitter[k];
+        if (ed.shape < 0 || ed.shape >= d.shapes || s.shape_emitter[ed.shape] >= 0) {
+            err = "scene descriptor: emitter " + std::to_string(k) + " names a bad or repeated shape";
+            return false;
+        }
+        if (!ed.cdf || ed.ncdf != s.shape_count[ed.shape] + 1) {
+            err = "scene descriptor: emitter " + std::to_string(k) + " needs a CDF of faces + 1 entries";
+            return false;
+        }
+        Emitter em;
+        em.shape = ed.shape;
+        em.area = ed.area;
+        for (int c = 0; c < 3; c++) em.radiance[c] = ed.radiance[c];
+        em.cdf.assign(ed.cdf, ed.cdf + ed.ncdf);
+        s.shape_emitter[ed.shape] = k;
+        s.emitters.push_back(std::move(em));
+    }
+    // The flattened Fast-BVH (bvh.h:102-105, :147-247): preorder, left child at
+    // i + 1, right child at i + rightOffset, leaves (rightOffset 0) covering
+    // build_prims[start, start + nPrims). Checked here: the layout, every
+    // triangle in exactly one leaf, and every child box inside its parent's box
+    // (the nesting the traversal's exactness argument needs).
+    const size_t nn = static_cast<size_t>(d.bvh_nodes);
+    s.order.assign(d.bvh_order, d.bvh_order + n);
+    std::vector<uint8_t> seen(n, 0);
+    for (size_t i = 0; i < n; i++) {
+        const int32_t t = s.order[i];
+        if (t < 0 || static_cast<size_t>(t) >= n || seen[t]) {
+            err = "scene descriptor: bvh_order is not a permutation of the triangles";
+            return false;
+        }
+        seen[t] = 1;
+    }
+    s.nodes.resize(nn);
+    for (size_t i = 0; i < nn; i++) {
+        const bdpt_bvh_node_desc& b = d.bvh[i];
+        FlatNode& f = s.nodes[i];
+        for (int a = 0; a < 3; a++) f.bmin[a] = b.bmin[a], f.bmax[a] = b.bmax[a];
+        f.start = b.start, f.nprims = b.nprims, f.right_offset = b.right_offset;
+    }
+    std::fill(seen.begin(), seen.end(), 0);
+    std::vector<uint8_t> visited(nn, 0);
+    struct Item {
+        size_t node;
+        int depth;
+    };
+    std::vector<Item> stack{{0, 0}};
+    size_t covered = 0, reached = 0;
+    s.max_depth = 0;
+    auto inside = [](const FlatNode& c, const FlatNode& p) {
+        for (int a = 0; a < 3; a++)
+            if (!(c.bmin[a] >= p.bmin[a] && c.bmax[a] <= p.bmax[a])) return false;
+        return true;
+    };
+    while (!stack.empty()) {
+        const Item it = stack.back();
+        stack.pop_back();
+        if (visited[it.node]) {
+            err = "scene descriptor: BVH node reached twice";
+            return false;
+        }
+        visited[it.node] = 1;
+        reached++;
+        s.max_depth = std::max(s.max_depth, it.depth);
+        const FlatNode& f = s.nodes[it.node];
+        if (f.right_offset == 0) {
+            if (f.nprims == 0 || f.start > n || f.nprims > n - f.start) {
+                err = "scene descriptor: BVH leaf " + std::to_string(it.node) + " has a bad triangle range";
+                return false;
+            }
+            for (uint32_t k = 0; k < f.nprims; k++) {
+                if (seen[f.start + k]++) {
+                    err = "scene descriptor: a triangle is in two BVH leaves";
+                    return false;
+                }
+            }
+            covered += f.nprims;
+            continue;
+        }
+        const size_t l = it.node + 1, r = it.node + f.right_offset;
+        if (f.right_offset < 2 || r >= nn || l >= nn) {
+            err = "scene descriptor: BVH node " + std::to_string(it.node) + " has a bad rightOffset";
+            return false;
+        }
+        if (!inside(s.nodes[l], f) || !inside(s.nodes[r], f)) {
+            err = "scene descriptor: BVH node " + std::to_string(it.node) + " has a child box outside its own box";
+            return false;
+        }
+        stack.push_back({r, it.depth + 1});
+        stack.push_back({l, it.depth + 1});
+    }
+    if (covered != n || reached != nn) {
+        err = "scene descriptor: the BVH leaves do not cover every triangle once, or nodes are unreachable";
+        return false;
+    }
     return true;
 }
 

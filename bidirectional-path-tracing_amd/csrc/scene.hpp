@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "bdpt_amd.h"
 #include "bdpt_types.h"
 
 namespace bdpt {
@@ -59,6 +60,11 @@ struct HostScene {
 // Returns false and sets `err` on failure (missing file, bad face index, face
 // without normal or material, bitmap textures, null BSDF on an emitter test).
 bool load_obj_scene(const std::string& obj_path, HostScene& out, std::string& err);
+
+// The same HostScene from the caller's in-memory Scene (core.h:352-358) handed
+// over as a bdpt_scene_desc: triangles, materials with their constructed
+// constants, emitters with their CDFs and the flattened Fast-BVH, validated.
+bool load_desc_scene(const bdpt_scene_desc& desc, HostScene& out, std::string& err);
 
 // Flattened arrays uploaded to HBM (layouts documented in bdpt_types.h).
 struct DeviceLayout {

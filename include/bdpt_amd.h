@@ -7,6 +7,8 @@
  *   bdpt_scene_load_obj      Scene::load                      src/core/renderer.cpp:235-315
  *                            (tinyobj LoadObj :249, BSDFs per illum :258-271,
  *                             emitters :279-305, AcceleratorBVH::build accel.h:115-123)
+ *   bdpt_scene_create        the Scene the Integrator holds (core.h:352-358: worldData, bsdfs,
+ *                            emitters, bvh) handed over from the caller's memory
  *   bdpt_camera_constants    camera set-up of Renderer::render renderer.cpp:140-153
  *                            and BDPTIntegrator bdpt.h:49-54, :485-489
  *   bdpt_ctx_create          Integrator::init (rgb allocation) src/core/integrator.cpp:16-20
@@ -99,13 +101,22 @@ typedef struct {
     bdpt_camera camera;
     int32_t width, height; /* [film] (the global image; shards still splat into it) */
     int32_t spp;           /* [renderer] spp */
-    int32_t rr_depth;      /* [renderer] rrDepth: hard path-depth cap (NO_RR=1, bdpt.h:18); 1..1024 */
+    int32_t rr_depth;      /* [renderer] rrDepth (bdpt.h:39): with russian_roulette 0 the hard path-depth
+                              cap (NO_RR = 1, bdpt.h:18), else where Russian roulette starts; 1..1024 */
     int32_t strategy;      /* BDPT_STRATEGY_* (reference default: BDPT) */
     uint32_t seed_base;    /* 260450963 = the reference's Sampler seed (renderer.cpp:155) */
     int32_t row_offset;    /* shard: render rows row_offset, row_offset+row_stride, ... */
     int32_t row_stride;    /*        (1 = whole image)                                   */
     uint32_t flags;        /* BDPT_FLAG_* */
+    int32_t russian_roulette; /* BDPT_RR_*: 0 = the reference as shipped (NO_RR 1, bdpt.h:18); 1 = its
+                                 NO_RR 0 branch (bdpt.h:68, :129-132, :188, :201-204) */
 } bdpt_frame_params;
+
+/* bdpt_frame_params.russian_roulette */
+#define BDPT_RR_NONE 0      /* NO_RR 1: every subpath stops at rrDepth (one draw at the cap) */
+#define BDPT_RR_LUMINANCE 1 /* NO_RR 0: past rrDepth a subpath continues while sampler.next() < rr, with
+                               rr = (luminance(throughput) < 0.01 ? 0.5 : 1) stored per vertex and entering
+                               every pdf (rr * pdf); no depth cap */
 
 #define BDPT_NUM_COUNTERS 32
 /* counters: [0] closest-hit rays, [1] shadow rays, [2] interior-node visits,
@@ -144,6 +155,63 @@ int bdpt_scene_export(const bdpt_scene* scene, float* tri_f32, int32_t* tri_i32,
  * (v0|ref index bits, e1|ref leaf id bits, e2|0), lbox[bvh_leaves][8] (lo|0 hi|0),
  * root_link. Any pointer may be NULL. */
 int bdpt_scene_export_traversal(const bdpt_scene* scene, float* wnodes, float* wtri, float* lbox, uint32_t* root_link);
+
+/* ---- scene hand-over from the caller's in-memory Scene (src/core/core.h:352-358) ----
+ * What Scene::load built (renderer.cpp:235-315), as plain arrays: the caller
+ * flattens WorldData, its bsdfs, emitters and the AcceleratorBVH it already has
+ * (INTEGRATION.md §2 does it from the reference's own types); nothing is
+ * re-parsed or rebuilt, and the result is the same bdpt_scene the OBJ path
+ * gives for the same file (bit-identical device arrays, bdpt_scene_export_layout). */
+typedef struct {
+    int32_t illum;             /* tinyobj material_t::illum: 7 diffuse, 3 mirror, 6 glass, 8 mixture, 5 null,
+                                  anything else Phong (renderer.cpp:258-271) */
+    float kd[3], ks[3], ke[3], tf[3]; /* diffuse, specular, emission, transmittance */
+    float ns, ni;              /* shininess, ior */
+    float scale, spec_weight;  /* MixtureBSDF / PhongBSDF::scale, ::specularSamplingWeight as constructed
+                                  (mixture.h:39-46, phong.h:40-47); unused by the other kinds */
+    int32_t has_texture;       /* non-zero: a bitmap texture (diffuse_/specular_texname) — rejected */
+} bdpt_material_desc;
+typedef struct {
+    int32_t shape;             /* Emitter::shapeID */
+    float area;                /* Emitter::area */
+    float radiance[3];         /* Emitter::radiance */
+    int32_t ncdf;              /* faceAreaDistribution.cdf.size() (= the shape's faces + 1) */
+    const float* cdf;          /* faceAreaDistribution.cdf, normalized */
+} bdpt_emitter_desc;
+typedef struct {
+    float bmin[3], bmax[3];    /* BVHFlatNode::bbox.min / max (externals/bvh.h:102-105) */
+    uint32_t start, nprims, right_offset;
+} bdpt_bvh_node_desc;
+typedef struct {
+    int64_t triangles;         /* AcceleratorBVH::objects.size() */
+    const float* positions;    /* [triangles][9] v0 v1 v2, shape by shape, faces in mesh.indices order
+                                  (the order AcceleratorBVH::build creates its objects, accel.h:115-123) */
+    const float* normals;      /* [triangles][9] the corners' normals (attrib.normals[normal_index]) */
+    const int32_t* tri_shape;  /* [triangles] shapeID */
+    const int32_t* tri_prim;   /* [triangles] primID = faceID / 3 */
+    const int32_t* tri_mat;    /* [triangles] mesh.material_ids[primID] */
+    int32_t shapes;            /* worldData.shapes.size() */
+    int32_t materials;         /* worldData.materials.size() = bsdfs.size() */
+    const bdpt_material_desc* material;
+    int32_t emitters;          /* Scene::emitters.size() */
+    const bdpt_emitter_desc* emitter;
+    int64_t bvh_nodes;         /* nodes of BVH::flatTree reachable from the root (preorder) */
+    const bdpt_bvh_node_desc* bvh;
+    const int32_t* bvh_order;  /* [triangles]: the triangle (index into the arrays above) that
+                                  AcceleratorBVH::objects[i] (= BVH::build_prims[i] after the build) is */
+} bdpt_scene_desc;
+/* Validates the descriptor (order, ranges, the BVH's layout and box nesting) and
+ * copies it; the caller's arrays may be freed afterwards. BDPT_ERR_INVALID with a
+ * message when it is inconsistent. */
+int bdpt_scene_create(const bdpt_scene_desc* desc, bdpt_scene** out);
+/* The scene's device arrays as uploaded by bdpt_ctx_create, for
+ * checking that two ingest paths agree bit for bit: 0 tri, 1 shade, 2 nodes (the
+ * reference's binary tree), 3 wnodes, 4 wtri, 5 lbox, 6 BSDF records, 7 emitter
+ * records, 8 emitter faces, 9 emitter CDFs, 10 shape -> emitter, 11 roots / tree
+ * sizes (uint32 root_link, wroot_link, wmax_stack, wdepth). *bytes = the array's
+ * size; dst may be NULL (size only), else it must hold *bytes on entry. */
+#define BDPT_LAYOUT_ARRAYS 12
+int bdpt_scene_export_layout(const bdpt_scene* scene, int32_t array, void* dst, int64_t* bytes);
 /* Camera constants: worldToCamera, cameraToWorld, cameraToClip, NDCToScreen
  * (column-major) then invWidth, invHeight, tan(fov/2), aspect, forward.xyz,
  * virtual near-plane distance — 72 floats. */
@@ -177,8 +245,10 @@ int bdpt_sampler_state(uint32_t seed, int64_t draws, uint32_t state[BDPT_MT19937
 /* BDPTIntegrator::render(ray, sampler) (bdpt.h:219-241): ray = o.xyz d.xyz min_t max_t;
  * `state` is the caller's sampler, advanced in place exactly as the reference
  * advances it. Returns Li; the camera splats of the sample's light subpath are
- * returned in order in splats[0 .. *nsplats) (at most rr_depth; BDPT_ERR_INVALID
- * if `capacity` is smaller than the count) for the caller to add to its image.
+ * returned in order in splats[0 .. *nsplats) for the caller to add to its image
+ * (at most rr_depth without Russian roulette). If `capacity` is smaller than the
+ * count: BDPT_ERR_INVALID, *nsplats = the count, `state` unchanged (call again
+ * with a larger list).
  * Any rr_depth in [1, 1024]. Synchronous. */
 int bdpt_render_sample_mt(bdpt_ctx* ctx, const bdpt_frame_params* params, const float ray[8],
                           uint32_t state[BDPT_MT19937_WORDS], float Li[3], bdpt_splat* splats, int32_t capacity,

@@ -153,3 +153,57 @@ def test_ingest_matches_oracle_with_many_materials(tmp_path):
     assert s.info()["materials"] == 408
     kinds = {s.bsdf_type(i)[1] for i in range(408)}
     assert kinds == {1, 2, 3, 4}
+
+
+# ---- bdpt_scene_create: the scene handed over from the caller's in-memory Scene
+def _layout(scene):
+    return [scene.export_layout(i) for i in range(len(bdpt_amd.LAYOUT_ARRAYS))]
+
+
+@pytest.mark.parametrize("scene_name", ["cbox_low", "caustic", "hardlight_mirror"])
+def test_scene_desc_round_trip_is_bit_identical(scene_name):
+    """A descriptor rebuilt from a loaded scene's exports (triangles back in
+    (shape, face) order, the BVH's object order, materials / emitters from the
+    device records) gives every device array bit for bit. The reference's own
+    Scene is the source in tests/test_adapter_cpu.py."""
+    s = bdpt_amd.Scene(variants.obj_path(scene_name))
+    d = s.to_desc()
+    t = bdpt_amd.Scene.from_desc(d)
+    assert _layout(t) == _layout(s)
+    assert t.info() == s.info()
+
+
+def _bad(d, **change):
+    import dataclasses
+    return dataclasses.replace(d, **change)
+
+
+def test_scene_desc_is_validated():
+    s = bdpt_amd.Scene(variants.obj_path("cbox_low"))
+    d = s.to_desc()
+    n = d.tri_shape.size
+    cases = {
+        "not (shape, face) order": _bad(d, tri_shape=d.tri_shape[::-1].copy()),
+        "primID not the face index": _bad(d, tri_prim=np.zeros(n, np.int32)),
+        "material out of range": _bad(d, tri_mat=np.full(n, len(d.materials), np.int32)),
+        "order not a permutation": _bad(d, bvh_order=np.zeros(n, np.int32)),
+        "emitter CDF length": _bad(d, emitters=[dict(d.emitters[0], cdf=d.emitters[0]["cdf"][:-1])]),
+        "repeated emitter shape": _bad(d, emitters=[d.emitters[0], d.emitters[0]]),
+        "texture": _bad(d, materials=[dict(d.materials[0], has_texture=1)] + d.materials[1:]),
+    }
+    bvh = d.bvh.copy()
+    root = bvh[0]["right_offset"]
+    bvh[1]["bmax"] = bvh[0]["bmax"] + 1.0  # a child box outside its parent's box
+    cases["child box outside parent"] = _bad(d, bvh=bvh)
+    bvh = d.bvh.copy()
+    bvh[0]["right_offset"] = len(bvh) + 5
+    cases["rightOffset out of range"] = _bad(d, bvh=bvh)
+    leaf = int(np.nonzero(d.bvh["right_offset"] == 0)[0][0])
+    bvh = d.bvh.copy()
+    bvh[leaf]["nprims"] = 0
+    cases["empty leaf"] = _bad(d, bvh=bvh)
+    assert root > 0
+    for what, bad in cases.items():
+        with pytest.raises(bdpt_amd.BdptError, match="descriptor|texture"):
+            bdpt_amd.Scene.from_desc(bad)
+            pytest.fail(what)
