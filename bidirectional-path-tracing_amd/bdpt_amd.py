@@ -33,6 +33,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BDPT_AMD_LIB") or os.path.join(HERE, "lib", "libbdpt_amd.so")
 
 STRATEGY_BDPT, STRATEGY_LIGHT_TRACING, STRATEGY_PATH_TRACING = 0, 1, 2
+RR_NONE, RR_LUMINANCE = 0, 1  # bdpt_frame_params.russian_roulette (BDPT_RR_*)
 FLAG_COUNT, FLAG_FULL_TRAVERSAL = 1, 2
 REFERENCE_SEED = 260450963  # renderer.cpp:155
 COUNTER_NAMES = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
@@ -165,7 +166,8 @@ BVH_NODE_DTYPE = np.dtype([("bmin", "<f4", 3), ("bmax", "<f4", 3), ("start", "<u
 
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
-                ("counters", ctypes.c_int64 * len(COUNTER_NAMES))]  # BDPT_NUM_COUNTERS
+                ("counters", ctypes.c_int64 * len(COUNTER_NAMES)),  # BDPT_NUM_COUNTERS
+                ("capped_samples", ctypes.c_int64)]
 
 
 # Sources that make up the frame kernels' code objects: their hash stamps the
@@ -292,8 +294,9 @@ class Config:
     height: int = 576
     spp: int = 1       # main.cpp:112
     rr_depth: int = 5  # main.cpp:105
-    rr_prob: float = 0.0  # read but unused: NO_RR = 1 (bdpt.h:18)
+    rr_prob: float = 0.0  # read but unused by bdpt.h (its rrProbability is luminance-based, bdpt.h:127-129)
     strategy: int = STRATEGY_BDPT
+    russian_roulette: int = 0  # RR_NONE: NO_RR = 1 as shipped (bdpt.h:18); RR_LUMINANCE: its NO_RR = 0 branch
     seed_base: int = REFERENCE_SEED
 
 
@@ -608,6 +611,7 @@ class BDPTIntegrator:
         p.width, p.height, p.spp, p.rr_depth = c.width, c.height, c.spp, c.rr_depth
         p.strategy, p.seed_base = c.strategy, c.seed_base & 0xFFFFFFFF
         p.row_offset, p.row_stride, p.flags = row_offset, row_stride, flags
+        p.russian_roulette = c.russian_roulette
         return p
 
     def render(self, ray: Ray, sampler: Sampler) -> np.ndarray:
@@ -631,7 +635,12 @@ class BDPTIntegrator:
         Li = (ctypes.c_float * 3)()
         p = self.params()
         st = np.ascontiguousarray(sampler.state, np.uint32)
-        _check(lib().bdpt_render_sample_mt(self._h, ctypes.byref(p), r, st.ctypes.data, Li, sp, cap, ctypes.byref(n)))
+        rc = lib().bdpt_render_sample_mt(self._h, ctypes.byref(p), r, st.ctypes.data, Li, sp, cap, ctypes.byref(n))
+        if rc == -1 and n.value > cap:  # Russian roulette: more splats than rr_depth; the state is untouched
+            cap = n.value
+            sp = (_Splat * cap)()
+            rc = lib().bdpt_render_sample_mt(self._h, ctypes.byref(p), r, st.ctypes.data, Li, sp, cap, ctypes.byref(n))
+        _check(rc)
         sampler.state = st
         return np.array(Li[:], np.float32), [(sp[k].pixel, np.array(sp[k].rgb[:], np.float32)) for k in range(n.value)]
 
@@ -692,7 +701,7 @@ class BDPTIntegrator:
         s = _Stats()
         _check(lib().bdpt_get_stats(self._h, ctypes.byref(s)))
         return dict(kernel_ms=s.kernel_ms, samples=s.samples, launches=s.launches,
-                    counters=dict(zip(COUNTER_NAMES, list(s.counters))))
+                    counters=dict(zip(COUNTER_NAMES, list(s.counters))), capped_samples=s.capped_samples)
 
     def synchronize(self) -> None:
         _check(lib().bdpt_synchronize(self._h))

@@ -50,6 +50,11 @@ hipError_t launch_frame_hbm(const dev::DevScene& sc, const dev::DevFrame& fr, fl
                             uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
                             hipStream_t stream, void* dparams);
 int frame_kernel_blocks_per_cu_hbm(size_t dyn_lds);
+// bdpt_kernels_rr.hip: the same megakernel with Russian roulette (NO_RR = 0)
+hipError_t launch_frame_rr(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                           uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
+                           hipStream_t stream, void* dparams);
+int frame_kernel_blocks_per_cu_rr(size_t dyn_lds);
 size_t pt_params_bytes();
 int pt_blocks_per_cu(size_t dyn_lds);
 hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8], float* fb,
@@ -78,6 +83,12 @@ int fail(int code, const std::string& msg) {
 
 constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
 constexpr int kMaxRrDepth = 1024;  // beyond 28 the megakernel continues MT19937 from an HBM ring
+// Russian roulette (NO_RR = 0): subpaths are unbounded in the reference; here a
+// subpath that reaches this depth ends and the sample is counted as capped (the
+// render then fails rather than return a different image). The light-vertex
+// store holds kRrDepthCap - 1 vertices per lane slot (64 B each).
+constexpr int kRrDepthCap = 256;
+constexpr int kRrMaxRrDepth = 192;
 }  // namespace
 
 // Error reporting shared with the other C-ABI translation units (exr_io.cpp, toml_config.cpp).
@@ -133,7 +144,8 @@ struct bdpt_ctx {
     float4* pt_levels = nullptr;
     size_t pt_levels_f4 = 0;
     uint32_t* pt_ring = nullptr;
-    uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28)
+    uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28, RR)
+    uint32_t* capped = nullptr;   // samples that reached kRrDepthCap (Russian roulette), per call
     void* pt_dparams = nullptr;
     // single-sample calls: the caller's std::mt19937 state and the splat list
     uint32_t* mt_state = nullptr;  // BDPT_MT19937_WORDS
@@ -321,7 +333,7 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
     for (void* p : {static_cast<void*>(c->work), static_cast<void*>(c->counters), static_cast<void*>(c->lv),
                     static_cast<void*>(c->gstack), static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams,
                     static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
-                    static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state),
+                    static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state), static_cast<void*>(c->capped),
                     static_cast<void*>(c->splat_list)})
         if (p) (void)hipFree(p);
     if (c->last_use) (void)hipEventDestroy(c->last_use);
@@ -422,6 +434,8 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     HIP_TRY(hipMalloc(&c->work, sizeof(unsigned long long)));
     HIP_TRY(hipMalloc(&c->counters, sizeof(unsigned long long) * BDPT_NUM_COUNTERS));
     HIP_TRY(hipMalloc(&c->sample_out, 16 * sizeof(float)));
+    HIP_TRY(hipMalloc(&c->capped, sizeof(uint32_t)));
+    HIP_TRY(hipMemset(c->capped, 0, sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&c->dparams, frame_params_bytes()));
     // Persistent grid: exactly the resident blocks (no co-residency is assumed:
     // the work queue has no inter-block waits, extra blocks would just queue).
@@ -450,7 +464,11 @@ static int check_params(const bdpt_frame_params* p) {
         return fail(BDPT_ERR_UNSUPPORTED, "unknown flag (bit 2, the round-1 wavefront schedule, was removed)");
     if (p->strategy < 0 || p->strategy > 2) return fail(BDPT_ERR_INVALID, "unknown strategy");
     if (p->row_stride < 1 || p->row_offset < 0) return fail(BDPT_ERR_INVALID, "bad row shard");
-    if (p->russian_roulette != BDPT_RR_NONE) return fail(BDPT_ERR_UNSUPPORTED, "russian_roulette mode not built");
+    if (p->russian_roulette != BDPT_RR_NONE && p->russian_roulette != BDPT_RR_LUMINANCE)
+        return fail(BDPT_ERR_INVALID, "unknown russian_roulette mode");
+    if (p->russian_roulette == BDPT_RR_LUMINANCE && p->rr_depth > kRrMaxRrDepth)
+        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 192 with Russian roulette (subpaths are bounded at 256 "
+                                          "vertices) is not supported");
     return BDPT_OK;
 }
 
@@ -464,11 +482,14 @@ static dev::DevFrame make_frame(const bdpt_frame_params* p) {
     fr.nrows = p->row_offset >= p->height ? 0 : (p->height - p->row_offset + p->row_stride - 1) / p->row_stride;
     fr.flags = p->flags;
     fr.total_samples = static_cast<uint64_t>(fr.nrows) * static_cast<uint64_t>(p->width) * p->spp;
+    fr.rr_mode = p->russian_roulette == BDPT_RR_LUMINANCE ? 1 : 0;
+    fr.depth_cap = fr.rr_mode ? kRrDepthCap : p->rr_depth;
+    fr.capped = nullptr;  // the context's word, set by the caller
     return fr;
 }
 
-static int ensure_lv(bdpt_ctx* c, int rr_depth, uint32_t nslots) {
-    const size_t need = static_cast<size_t>(std::max(rr_depth - 1, 1)) * light_vertex_fields() * nslots;
+static int ensure_lv(bdpt_ctx* c, int depth_bound, uint32_t nslots) {
+    const size_t need = static_cast<size_t>(std::max(depth_bound - 1, 1)) * light_vertex_fields() * nslots;
     if (need > c->lv_floats) {
         if (c->lv) HIP_TRY(hipFree(c->lv));
         c->lv = nullptr;
@@ -510,16 +531,18 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-    const dev::DevFrame fr = make_frame(p);
+    dev::DevFrame fr = make_frame(p);
+    fr.capped = c->capped;
     const bool hbm = c->sc.lds_bsdf_off == dev::kNoLds;
+    const bool rr = fr.rr_mode != 0;
     const float* eye[1] = {p->camera.eye};
-    if (hbm && p->rr_depth > kLazyRrDepth)
-        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 with BSDF records in HBM (too many materials for the LDS "
-                                          "table) is not built");
-    if ((rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
+    if (hbm && (p->rr_depth > kLazyRrDepth || rr))
+        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 or Russian roulette with BSDF records in HBM (too many "
+                                          "materials for the LDS table) is not built");
+    if ((rc = ensure_lv(c, fr.depth_cap, c->nslots))) return rc;
     dev::DevScene sc = c->sc;
     sc.node_slack = node_slack_needed(c, eye, 1);
-    if (p->rr_depth > kLazyRrDepth) {  // draws past 226: the lanes' MT19937 rings
+    if (p->rr_depth > kLazyRrDepth || rr) {  // draws past 226: the lanes' MT19937 rings
         if (!c->mt_ring) HIP_TRY(hipMalloc(&c->mt_ring, sizeof(uint32_t) * 624 * static_cast<size_t>(c->nslots)));
         sc.mt_ring = c->mt_ring;
         sc.mt_ring_stride = c->nslots;
@@ -527,10 +550,16 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
+    HIP_TRY(hipMemsetAsync(c->capped, 0, sizeof(uint32_t), st));
     HIP_TRY(hipEventRecord(c->ev0, st));
     int64_t launches = 0;
     if (fr.total_samples > 0) {
-        if (p->rr_depth > kLazyRrDepth) {  // never more resident blocks than the slots allocated
+        if (rr) {  // never more resident blocks than the slots allocated
+            const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_rr(
+                                                           4 * static_cast<size_t>(c->sc.lds_words)));
+            HIP_TRY(launch_frame_rr(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
+                                    c->dparams));
+        } else if (p->rr_depth > kLazyRrDepth) {  // never more resident blocks than the slots allocated
             const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_deep(
                                                            4 * static_cast<size_t>(c->sc.lds_words)));
             HIP_TRY(launch_frame_deep(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
@@ -846,6 +875,9 @@ int bdpt_get_stats(bdpt_ctx* c, bdpt_stats* out) {
         unsigned long long host[BDPT_NUM_COUNTERS];
         HIP_TRY(hipMemcpy(host, c->counters, sizeof(host), hipMemcpyDeviceToHost));
         for (int i = 0; i < BDPT_NUM_COUNTERS; i++) c->stats.counters[i] = static_cast<int64_t>(host[i]);
+        uint32_t capped = 0;
+        HIP_TRY(hipMemcpy(&capped, c->capped, sizeof(capped), hipMemcpyDeviceToHost));
+        c->stats.capped_samples = capped;
         c->pending_timing = false;
     }
     *out = c->stats;
@@ -880,6 +912,14 @@ int bdpt_render_host(bdpt_ctx* c, const bdpt_frame_params* p, float* fb_host) {
     if ((rc = bdpt_render(c, p, c->tmp_fb, c->stream))) return rc;
     HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (p->russian_roulette) {
+        bdpt_stats st;
+        if ((rc = bdpt_get_stats(c, &st))) return rc;
+        if (st.capped_samples)
+            return fail(BDPT_ERR_UNSUPPORTED, std::to_string(st.capped_samples) +
+                                                  " samples had a subpath reach the 256-vertex bound of Russian "
+                                                  "roulette; the image is not the reference's");
+    }
     return BDPT_OK;
 }
 
@@ -891,11 +931,12 @@ static int render_bdpt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const flo
     if (rc) return rc;
     if ((rc = check_mt_state(state))) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    if ((rc = ensure_lv(c, p->rr_depth, c->nslots))) return rc;
+    if ((rc = ensure_lv(c, p->russian_roulette ? kRrDepthCap : p->rr_depth, c->nslots))) return rc;
     // a sample splats at most once per light vertex: rr_depth bounds the list
     // without Russian roulette; with it the list grows on demand (below)
     if ((rc = ensure_sample_buffers(c, std::max(p->rr_depth, 1)))) return rc;
-    const dev::DevFrame fr = make_frame(p);
+    dev::DevFrame fr = make_frame(p);
+    fr.capped = c->capped;
     dev::DevScene sc = c->sc;
     sc.mt_ring = c->mt_state;  // the sample kernel's generator state (mt_state_u32)
     const float* origins[2] = {p->camera.eye, ray};  // camera connections start at the eye, the walk at ray.o
@@ -911,14 +952,19 @@ static int render_bdpt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const flo
         HIP_TRY(hipMemcpyAsync(c->mt_state, state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyHostToDevice,
                                c->stream));
         HIP_TRY(hipMemcpyAsync(c->splat_list, hdr, sizeof(hdr), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemsetAsync(c->capped, 0, sizeof(uint32_t), c->stream));
         HIP_TRY(launch_sample(sc, fr, c->splat_list, c->lv, c->gstack, r, c->sample_out, c->stream));
         list.assign(4 * (static_cast<size_t>(c->splat_cap) + 1), 0.f);
         HIP_TRY(hipMemcpyAsync(out, c->sample_out, sizeof(out), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(list.data(), c->splat_list, list.size() * sizeof(float), hipMemcpyDeviceToHost,
                                c->stream));
         HIP_TRY(hipMemcpyAsync(st_out, c->mt_state, sizeof(st_out), hipMemcpyDeviceToHost, c->stream));
+        uint32_t capped = 0;
+        HIP_TRY(hipMemcpyAsync(&capped, c->capped, sizeof(capped), hipMemcpyDeviceToHost, c->stream));
         if ((rc = end_use(c, c->stream))) return rc;
         HIP_TRY(hipStreamSynchronize(c->stream));
+        if (capped)
+            return fail(BDPT_ERR_UNSUPPORTED, "a subpath reached the 256-vertex bound of Russian roulette");
         std::memcpy(&n, &list[0], 4);
         if (n <= static_cast<uint32_t>(c->splat_cap)) break;
         // more splats than the device list holds (the kernel counts them all):

@@ -144,6 +144,9 @@ struct DevFrame {
     int32_t row_offset, row_stride, nrows;
     uint32_t flags;
     uint64_t total_samples;  // nrows * W * spp
+    int32_t rr_mode;    // 1: NO_RR = 0 (Russian roulette past rr_depth; the bdpt_kernels_rr.hip build)
+    int32_t depth_cap;  // subpath depth bound: rr_depth under NO_RR; the light-vertex store's bound with RR
+    uint32_t* capped;   // samples whose subpath reached depth_cap with RR on (then not the reference's)
 };
 
 struct Ray {

@@ -19,8 +19,39 @@ constexpr int kLvFields = 16;    // p vcm n vc wo rr tp mat
 constexpr uint32_t kFlagNoEyeAccum = 0x100u;  // single-sample API: Li is returned, not added
 // Safety bound on the queries of one sample: a legal sample issues at most D
 // light-walk rays, D camera splats, D eye-walk rays and, per eye vertex, one
-// light sample plus D - 1 connections: < (D + 3)(D + 1) for rrDepth D.
-__device__ __forceinline__ int max_steps_per_sample(int rr_depth) { return (rr_depth + 3) * (rr_depth + 1) + 64; }
+// light sample plus D - 1 connections: < (D + 3)(D + 1) for a depth bound D
+// (rrDepth, or DevFrame::depth_cap with Russian roulette).
+__device__ __forceinline__ int max_steps_per_sample(int depth_bound) {
+    return (depth_bound + 3) * (depth_bound + 1) + 64;
+}
+
+// ---------------------------------------------------------- Russian roulette
+// The reference ships with NO_RR = 1 (bdpt.h:18): every subpath stops at
+// rrDepth and every stored rr is 1. Its NO_RR = 0 branch continues past rrDepth
+// while sampler.next() < rrProbability (bdpt.h:68, :188), with rrProbability =
+// (depth + 1) < rrDepth ? 1 : (getLuminance(throughput) < 0.01 ? 0.5 : 1)
+// (bdpt.h:129, :201) stored in the vertex and multiplying every pdf of it
+// (bdpt.h:250, :272, :342, :410, :417, :461-472). BDPT_RR 0: the NO_RR = 1
+// builds (rr is the constant 1, nothing of it is compiled); 1: the RR build of
+// the megakernel (bdpt_kernels_rr.hip); 2: chosen per launch (DevFrame::rr_mode,
+// the single-sample build).
+#ifndef BDPT_RR
+#define BDPT_RR 0
+#endif
+__device__ __forceinline__ bool rr_on(const DevFrame& fr) {
+#if BDPT_RR == 1
+    return true;
+#elif BDPT_RR == 2
+    return fr.rr_mode != 0;
+#else
+    (void)fr;
+    return false;
+#endif
+}
+__device__ __forceinline__ float rr_probability(const DevFrame& fr, int depth, f3 tp) {
+    if (!rr_on(fr) || (depth + 1) < fr.rr_depth) return 1.f;
+    return dot(tp, mk(0.212671f, 0.715160f, 0.072169f)) < 0.01f ? 0.5f : 1.f;  // getLuminance (math.h:56-58)
+}
 
 // Light-vertex scratch, one contiguous record per lane: vertex v of slot s is
 // the four float4 at lv[(s * maxv + v) * 4 + q] — (p, vcm) (n, vc) (wo, rr)
@@ -37,9 +68,9 @@ __device__ __forceinline__ LightStore light_store(float* lv, int rr_depth, uint3
     return LightStore{reinterpret_cast<float4*>(lv), static_cast<uint32_t>(rr_depth > 1 ? rr_depth - 1 : 1), slot};
 }
 
-struct Vertex {  // PathVertex (bdpt.h:24-35); its Frame is rebuilt from n where used, rr is 1 (NO_RR)
+struct Vertex {  // PathVertex (bdpt.h:24-35); its Frame is rebuilt from n where used
     f3 p, n, wo, tp;
-    float vcm, vc;
+    float vcm, vc, rr;
     int mat;
 };
 
@@ -76,7 +107,7 @@ __device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
     Vertex x;
     x.p = xyz(a), x.vcm = a.w;
     x.n = xyz(b), x.vc = b.w;
-    x.wo = xyz(c);  // c.w: the vertex's rr, always 1 under NO_RR (bdpt.h:18): x * rr == x
+    x.wo = xyz(c), x.rr = c.w;  // rr: always 1 under NO_RR (bdpt.h:18), where x * rr == x is not formed
     x.tp = xyz(d), x.mat = __float_as_int(d.w);
     return x;
 }
@@ -88,8 +119,7 @@ __device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
 // ContinuePathRandomWalk (bdpt.h:243-291): BSDF sample (2 draws), throughput,
 // vc / vcm recursion (Georgiev VCM Eqs. 52-54) and the next ray.
 __device__ __forceinline__ bool continue_walk(const BsdfRecord& b, const Hit& h, LazyMT& rng, f3& tp, int& depth,
-                                              float& vc, float& vcm, Ray& ray) {
-    const float rrp = 1.f;  // NO_RR (bdpt.h:18)
+                                              float& vc, float& vcm, Ray& ray, float rrp) {
     const bool delta = is_delta(b);
     float pdf;
     f3 wi;
@@ -205,7 +235,7 @@ struct LaneCold {
     int ci;       // next light vertex to connect
     int depth;
     uint32_t pure;  // isPathPureSpecular
-    uint32_t pad_;  // keeps the record an odd number of dwords
+    float rr;       // rrProbability of the current vertex (Russian-roulette builds; keeps the record odd-dword)
 };
 static_assert(sizeof(LaneCold) == 92, "odd dword stride keeps LDS accesses conflict free");
 
@@ -294,6 +324,20 @@ __device__ __forceinline__ void tally_action(Counts& cnt, bool on) {
     }
 }
 
+// The subpath loop test of bdpt.h:68 / :188. With Russian roulette a subpath
+// that reaches DevFrame::depth_cap (the light-vertex store's bound) ends there
+// and the sample is counted in *capped (the frame is then not the reference's).
+__device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
+    if (L.c.depth < fr.rr_depth) return true;
+    const float u = next1(L.rng);
+    if (!rr_on(fr) || !(u < L.c.rr)) return false;
+    if (L.c.depth >= fr.depth_cap) {
+        atomicAdd(fr.capped, 1u);
+        return false;
+    }
+    return true;
+}
+
 template <bool COUNT>
 __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
                         const LightStore& ls, Counts& cnt) {
@@ -315,6 +359,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         L.c.vcm = static_cast<float>(fr.W * fr.H) * rcp_cr(t1Pdf);
         L.c.depth = 1;
         L.c.pure = 1u;
+        if (rr_on(fr)) L.c.rr = 1.f;  // rrProbability before the first vertex (bdpt.h:65)
         L.c.Li = mk(0.f, 0.f, 0.f);
         L.ray = Ray{cam_o, L.c.cam_d, 1.f, 1000.f};
         act = A_EYE_NEXT;
@@ -357,6 +402,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             act = A_FINISH;
             break;
         }
+        if (rr_on(fr)) L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);  // bdpt.h:129-134
         if (is_delta(b)) {
             act = A_EYE_CONTINUE;
             break;
@@ -388,6 +434,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         L.c.vcm = div_cr(areaPdf, emissionPdf);
         L.c.nl = 0;
         L.c.depth = 1;
+        if (rr_on(fr)) L.c.rr = 1.f;  // bdpt.h:187
         if (edir.z <= 0.f) {  // bdpt.h:179-182 (the eye subpath follows)
             L.state = ST_DEFER;
             act = A_ISSUED;
@@ -417,8 +464,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
         const f3 Li = ((ep.f * rcp_cr(pdf_w)) * L.c.tp) * ld3(e.radiance);
         if (is_zero(Li)) break;
-        const float lightWeight = div_cr(ep.fwd * 1.f, pdf_w);
-        const float eyePrevRev = ep.rev * 1.f;
+        const float rrE = rr_on(fr) ? L.c.rr : 1.f;  // eyeVertex.rr (bdpt.h:410, :417)
+        const float lightWeight = div_cr(ep.fwd * rrE, pdf_w);
+        const float eyePrevRev = ep.rev * rrE;
         const float eyeCurRev_a = cosAtEye * rcp_cr(d2) * kInvTwoPi;
         const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
         const float mis = rcp_cr(lightWeight + 1.f + eyeWeight);
@@ -433,6 +481,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         L.c.vcm *= div_cr(dist2, absCosIn);
         L.c.vc *= rcp_cr(absCosIn);
         act = A_LIGHT_CONTINUE;
+        if (rr_on(fr)) L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);  // bdpt.h:201-204
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         if (is_delta(b)) break;
         // connectToCamera (bdpt.h:295-371): everything but the visibility test.
@@ -466,7 +515,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         rad = rad * rcp_cr(nlight);
         rad = rad * rcp_cr(static_cast<float>(fr.spp));
         const float reversePdf_a = 1.f * img2surf;
-        const float prevRev = ep.rev * 1.f;  // swapped (wi, wo), rr = 1
+        const float prevRev = ep.rev * (rr_on(fr) ? L.c.rr : 1.f);  // swapped (wi, wo) * lightVertex.rr (bdpt.h:342)
         const float lightWeight = div_cr(reversePdf_a, nlight) * (L.c.vcm + prevRev * L.c.vc);
         const float mis = rcp_cr(lightWeight + 1.f + 0.f);
         L.c.pend = (fr.strategy == 0) ? rad * mis : rad;
@@ -508,10 +557,11 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             const EvalPdfs eL = bsdf_eval_pdfs(bl, wiL, V.wo), eE = bsdf_eval_pdfs(be, wiE, L.h.wo);
             f3 Li = eL.f * eE.f;
             Li = Li * ((V.tp * L.c.tp) * invD2);
-            const float eyePathRev_w = eL.fwd * 1.f;  // * vertex rr (1)
-            const float lightPrevRev = eL.rev * 1.f;
-            const float lightPathRev_w = eE.fwd * 1.f;
-            const float eyePrevRev = eE.rev * 1.f;
+            const float rrL = rr_on(fr) ? V.rr : 1.f, rrE = rr_on(fr) ? L.c.rr : 1.f;  // bdpt.h:461-472
+            const float eyePathRev_w = eL.fwd * rrL;
+            const float lightPrevRev = eL.rev * rrL;
+            const float lightPathRev_w = eE.fwd * rrE;
+            const float eyePrevRev = eE.rev * rrE;
             const float lightPathRev_a = lightPathRev_w * cosL * invD2;
             const float eyePathRev_a = eyePathRev_w * cosE * invD2;
             const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
@@ -529,8 +579,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const bool light = act == A_LIGHT_CONTINUE;
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         const bool delta = is_delta(b);
-        if (light && !delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, 1.f);  // the pre-walk state
-        const bool more = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray);
+        const float rrp = rr_on(fr) ? L.c.rr : 1.f;
+        if (light && !delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, rrp);  // the pre-walk state
+        const bool more = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, rrp);
         if (!light) {
             act = more ? A_EYE_NEXT : A_FINISH;
         } else if (more) {
@@ -544,22 +595,18 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             act = A_ISSUED;
         }
     } BDPT_END;
-    BDPT_ACTION(29, act == A_LIGHT_NEXT) {  // loop condition (bdpt.h:188); NO_RR still draws once at the cap
-        if (!(L.c.depth < fr.rr_depth)) {
-            (void)next1(L.rng);
-            L.state = ST_DEFER;  // the eye subpath starts next step
-        } else {
-            L.state = ST_LIGHT;
-        }
+    // Loop conditions `depth < m_rrDepth || (sampler.next() < rrProbability && !NO_RR)`
+    // (bdpt.h:188, :68): past rrDepth one draw, then (RR only) a continuation.
+    BDPT_ACTION(29, act == A_LIGHT_NEXT) {
+        L.state = walk_continues(L, fr) ? ST_LIGHT : ST_DEFER;  // ST_DEFER: the eye subpath starts next step
         act = A_ISSUED;
     } BDPT_END;
-    BDPT_ACTION(30, act == A_EYE_NEXT) {  // bdpt.h:68
-        if (!(L.c.depth < fr.rr_depth)) {
-            (void)next1(L.rng);
-            act = A_FINISH;
-        } else {
+    BDPT_ACTION(30, act == A_EYE_NEXT) {
+        if (walk_continues(L, fr)) {
             L.state = ST_EYE;
             act = A_ISSUED;
+        } else {
+            act = A_FINISH;
         }
     } BDPT_END;
     BDPT_ACTION(31, act == A_FINISH) {
@@ -643,7 +690,7 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
         default: act = A_DONE;
     }
     // A state-machine bug must not hang the GPU: bound the queries per sample.
-    if (++L.c.steps > max_steps_per_sample(fr.rr_depth) && act != A_FINISH) act = A_FINISH;
+    if (++L.c.steps > max_steps_per_sample(rr_on(fr) ? fr.depth_cap : fr.rr_depth) && act != A_FINISH) act = A_FINISH;
     return act;
 }
 

@@ -6,5 +6,6 @@
 // splats are returned as a list (splat_add, bdpt_path.hpp). Only the sample
 // kernels and their launchers exist in this translation unit.
 #define BDPT_SAMPLER_STATE 1
+#define BDPT_RR 2  // NO_RR 1 or 0 per launch (DevFrame::rr_mode)
 #include "bdpt_kernels.hip"
 #include "pt_kernels.hip"

@@ -137,6 +137,9 @@ typedef struct {
     int64_t samples;       /* camera samples rendered by the last call */
     int64_t launches;      /* kernel launches of the last call */
     int64_t counters[BDPT_NUM_COUNTERS];
+    int64_t capped_samples; /* Russian roulette: samples of the last call with a subpath that reached the
+                               256-vertex bound (the reference would have continued; > 0 means the frame
+                               is not the reference's, and bdpt_render_host fails) */
 } bdpt_stats;
 
 const char* bdpt_last_error(void);

@@ -39,6 +39,7 @@ class Params(ctypes.Structure):
         ("di_emitter_samples", ctypes.c_int),
         ("di_bsdf_samples", ctypes.c_int),
         ("seed_base", ctypes.c_uint32),
+        ("russian_roulette", ctypes.c_int),  # 0: NO_RR = 1 (bdpt.h:18, as shipped); 1: its NO_RR = 0 branch
     ]
 
 
@@ -96,6 +97,8 @@ def lib():
         L.tro_sample.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_void_p]
         L.tro_counters.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+        L.tro_rr_overflow.restype = ctypes.c_int64
+        L.tro_rr_overflow.argtypes = [ctypes.c_int]
         L.tro_mt19937_nth.restype = ctypes.c_uint32
         L.tro_mt19937_nth.argtypes = [ctypes.c_uint32, ctypes.c_int]
         L.tro_sampler_nth.restype = ctypes.c_float
@@ -109,7 +112,8 @@ def lib():
     return _lib
 
 
-def make_params(cam: dict, width: int, height: int, spp: int, rr_depth: int, strategy: int = 0) -> Params:
+def make_params(cam: dict, width: int, height: int, spp: int, rr_depth: int, strategy: int = 0,
+                russian_roulette: int = 0) -> Params:
     p = Params()
     p.eye[:] = [float(x) for x in cam["eye"]]
     p.at[:] = [float(x) for x in cam["at"]]
@@ -117,6 +121,7 @@ def make_params(cam: dict, width: int, height: int, spp: int, rr_depth: int, str
     p.fov = float(cam["fov"])
     p.width, p.height, p.spp, p.rr_depth = width, height, spp, rr_depth
     p.strategy = strategy
+    p.russian_roulette = russian_roulette
     p.seed_base = 260450963  # the reference's Sampler seed (renderer.cpp:155)
     return p
 

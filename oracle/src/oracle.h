@@ -40,6 +40,9 @@ typedef struct {
     /* per-(pixel, sample) seeds are seed_base + pixel*spp + k; the reference's
      * Sampler seed 260450963 (renderer.cpp:155) unless a test varies it */
     uint32_t seed_base;
+    /* 0: NO_RR = 1 (bdpt.h:18, the reference as shipped); 1: its NO_RR = 0 branch
+     * (Russian roulette past rrDepth, bdpt.h:68, :129-132, :188, :201-204) */
+    int russian_roulette;
 } tro_params;
 
 /* Loads an OBJ (+ MTL) exactly as Scene::load does (reference
@@ -78,6 +81,10 @@ void tro_sample(const tro_scene* s, const tro_params* p, int pixel, int k, float
  * [2] interior-node visits, [3] triangle tests, [4] light vertices stored,
  * [5] light-vertex reads in connections, [6] splats, [7] RNG draws. */
 void tro_counters(int64_t out[8], int reset);
+
+/* Light vertices dropped because a subpath outgrew the oracle's 1024-vertex
+ * store (Russian roulette only; always 0 in practice). */
+int64_t tro_rr_overflow(int reset);
 
 /* Unit-level hooks for KAT tests. */
 uint32_t tro_mt19937_nth(uint32_t seed, int n);   /* n-th raw output */

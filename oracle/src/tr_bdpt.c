@@ -12,7 +12,7 @@
  *   BSDFs            src/bsdfs/diffuse.h:35-61, perfectmirror.h:33-59,
  *                    glass.h:40-108, mixture.h:59-151, phong.h:56-100
  *   emitter helpers  src/core/integrator.cpp:46-100, math.h:107-111
- *   BDPT             src/integrators/bdpt.h:46-505 (NO_RR=1, BDPT strategy)
+ *   BDPT             src/integrators/bdpt.h:46-505 (NO_RR 1 or 0, BDPT / LT / PT strategy)
  *   driver           src/core/renderer.cpp:143-210 with per-(pixel, sample)
  *                    seeds (SURVEY.md §8(c) parity convention)
  */
@@ -673,7 +673,32 @@ static int continue_walk(const ctx_t* c, hit_t* h, tr_sampler* smp, float rrp, p
     return 1;
 }
 
-#define MAX_LIGHT_VERTS 64
+#define MAX_LIGHT_VERTS 1024 /* light vertices kept per sample (the reference's vector is unbounded;
+                                 a longer subpath is counted in g_ctr[7]'s overflow twin below) */
+static __thread int64_t g_rr_overflow;
+
+/* rrProbability (bdpt.h:127-132 / :199-204): 1 before rrDepth, then 0.5 when the
+ * throughput's luminance (getLuminance, math.h:56-58: a glm dot) is below 0.01;
+ * always 1 under NO_RR = 1 (bdpt.h:18, the reference as shipped). */
+static float rr_probability(const ctx_t* c, int depth, v3 tp) {
+    if (!c->p->russian_roulette) return 1.f;
+    if ((depth + 1) < c->rr_depth) return 1.f;
+    return vdot(tp, V3(0.212671f, 0.715160f, 0.072169f)) < 0.01f ? 0.5f : 1.f;
+}
+
+/* The loop test `depth < m_rrDepth || (sampler.next() < rrProbability && !NO_RR)`
+ * (bdpt.h:68, :188): past rrDepth one draw, then a continuation only with RR on. */
+static int walk_continues(const ctx_t* c, int depth, float rrp, tr_sampler* smp) {
+    if (depth < c->rr_depth) return 1;
+    const float u = s_next(smp);
+    return c->p->russian_roulette && u < rrp;
+}
+
+int64_t tro_rr_overflow(int reset) {
+    int64_t v = g_rr_overflow;
+    if (reset) g_rr_overflow = 0;
+    return v;
+}
 
 /* lightSubpathWalk (bdpt.h:158-217) */
 static int light_walk(const ctx_t* c, tr_sampler* smp, pvert_t* lverts) {
@@ -696,25 +721,25 @@ static int light_walk(const ctx_t* c, tr_sampler* smp, pvert_t* lverts) {
     if (edir.z <= 0.f) return 0;
     int depth = 1;
     float rrp = 1.f;
-    for (;;) {
-        if (!(depth < c->rr_depth)) {
-            (void)s_next(smp); /* (sampler.next() < rr && !NO_RR) is evaluated, then false */
-            break;
-        }
+    while (walk_continues(c, depth, rrp, smp)) {
         hit_t hit;
         if (!scene_intersect(s, &wi, &hit)) break;
         float distSquared = hit.t * hit.t;
         float absCosIn = fabsf(hit.wo.z);
         vcm *= (distSquared / absCosIn);
         vc *= (1.f / absCosIn);
-        rrp = 1.f;
+        rrp = rr_probability(c, depth, throughput);
         int delta = is_delta(bsdf_of(s, &hit));
         pvert_t lv = {hit, throughput, vcm, vc, rrp};
         if (!delta) connect_to_camera(c, &lv);
         if (!continue_walk(c, &hit, smp, rrp, &lv, &throughput, &depth, &vc, &vcm, &wi)) break;
-        if (!delta && nl < MAX_LIGHT_VERTS) {
-            lverts[nl++] = lv;
-            g_ctr[4]++;
+        if (!delta) {
+            if (nl < MAX_LIGHT_VERTS) {
+                lverts[nl++] = lv;
+                g_ctr[4]++;
+            } else {
+                g_rr_overflow++;
+            }
         }
     }
     return nl;
@@ -735,11 +760,7 @@ static v3 eye_walk(const ctx_t* c, const pvert_t* lverts, int nl, ray_t ray, tr_
     float vcm = (float)(c->W * c->H) * (1.f / t1Pdf);
     int depth = 1;
     float rrp = 1.f;
-    for (;;) {
-        if (!(depth < c->rr_depth)) {
-            (void)s_next(smp);
-            break;
-        }
+    while (walk_continues(c, depth, rrp, smp)) {
         hit_t hit;
         if (!scene_intersect(s, &wi, &hit)) break;
         float distSquared = hit.t * hit.t;
@@ -770,7 +791,7 @@ static v3 eye_walk(const ctx_t* c, const pvert_t* lverts, int nl, ray_t ray, tr_
             }
             break;
         }
-        rrp = 1.f;
+        rrp = rr_probability(c, depth, throughput);
         pvert_t ev = {hit, throughput, vcm, vc, rrp};
         if (!is_delta(bsdf_of(s, &hit))) {
             pureSpecular = 0;

@@ -30,6 +30,8 @@ import variants  # noqa: E402
 REF = os.path.join(REPO, "oracle", "_ref", "ref_bdpt")
 # the reference built with its compile-time strategy switch (bdpt.h:16-17) flipped (oracle/ref/Makefile)
 REF_STRATEGY = {"bdpt": REF, "lt": REF + "_lt", "pt": REF + "_pt"}
+# the reference built with NO_RR = 0 (bdpt.h:18 flipped, oracle/ref/Makefile): Russian roulette past rrDepth
+REF_RR = REF + "_rr"
 
 # name: (scene, W, H, spp, rrDepth, row_stride[, strategy: bdpt | lt (LIGHT_TRACING) | pt (PATH_TRACING)])
 FRAMEBUFFERS = {
@@ -48,6 +50,17 @@ FRAMEBUFFERS = {
     "G10_caustic_pt_64x64_spp16": ("caustic", 64, 64, 16, 8, 1, "pt"),
     "G11_hardlight_lt_64x64_spp16": ("hardlight", 64, 64, 16, 2, 1, "lt"),
     "G12_hardlight_pt_64x64_spp16": ("hardlight", 64, 64, 16, 2, 1, "pt"),
+}
+
+# The reference's Russian-roulette branch (NO_RR = 0): name: (scene, W, H, spp, rrDepth, row_stride)
+RR_FRAMEBUFFERS = {
+    "R1_caustic_rr_64x64_spp16": ("caustic", 64, 64, 16, 8, 1),
+    "R2_hardlight_rr_64x64_spp16": ("hardlight", 64, 64, 16, 2, 1),
+    "R3_cbox_low_rr_64x64_spp4": ("cbox_low", 64, 64, 4, 5, 1),
+    # roulette from the first bounce on (rrDepth 1: every loop test draws)
+    "R4_caustic_rr1_48x48_spp4": ("caustic", 48, 48, 4, 1, 1),
+    "R5_hardlight_mirror_rr_48x48_spp4": ("hardlight_mirror", 48, 48, 4, 3, 1),
+    "R6_caustic_rr_512x512_spp2_rows32": ("caustic", 512, 512, 2, 8, 32),
 }
 
 # PathTracerIntegrator (src/integrators/path.h) frames: name: (scene, W, H, spp, path settings)
@@ -111,7 +124,7 @@ def main() -> None:
         "framebuffers": dict(old.get("framebuffers", {})),
         "scenes": dict(old.get("scenes", {})),
     }
-    for sect in ("path_framebuffers", "direct_framebuffers", "large_framebuffers"):
+    for sect in ("rr_framebuffers", "path_framebuffers", "direct_framebuffers", "large_framebuffers"):
         if sect in old:
             manifest[sect] = dict(old[sect])
     tmp = tempfile.mkdtemp()
@@ -137,6 +150,27 @@ def main() -> None:
                                               mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
                                               ref_seconds=info["seconds"])
         print(name, manifest["framebuffers"][name]["sha256"][:16], info)
+    for name, (scene, W, H, spp, rr, stride) in RR_FRAMEBUFFERS.items():
+        if only and name not in only:
+            continue
+        toml = os.path.join(tmp, name + ".toml")
+        with open(toml, "w") as f:
+            f.write(variants.toml_text(scene, W, H, spp, rr))
+        out = os.path.join(tmp, name + ".f32")
+        cmd = [REF_RR, "render", toml, str(W), str(H), str(spp), "--rr", str(rr), "--out", out]
+        if stride > 1:
+            cmd += ["--row-stride", str(stride)]
+        r = subprocess.run(cmd, capture_output=True, text=True, check=True, timeout=3600)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        fb = np.fromfile(out, np.float32)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), fb=fb)
+        manifest.setdefault("rr_framebuffers", dict(old.get("rr_framebuffers", {})))
+        manifest["rr_framebuffers"][name] = dict(scene=scene, width=W, height=H, spp=spp, rr_depth=rr,
+                                                 row_stride=stride, russian_roulette=1, samples=info["samples"],
+                                                 sha256=sha(fb.tobytes()),
+                                                 mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
+                                                 ref_seconds=info["seconds"])
+        print(name, manifest["rr_framebuffers"][name]["sha256"][:16], info)
     for name, (scene, W, H, spp, path) in PATH_FRAMEBUFFERS.items():
         if only and name not in only:
             continue

@@ -99,3 +99,40 @@ def test_reference_cli_renders_bdpt_gpu_scene(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Render took:" in r.stdout
     assert toml.with_suffix(".exr").exists()
+
+
+# The same binding over the reference built with NO_RR = 0 (oracle/_ref/adapter/rr): the
+# adapter reads the macro (bdpt.h:18) and asks the library for Russian roulette.
+CHECK_RR = os.path.join(AD, "rr", "adapter_check")
+
+
+@pytest.mark.parametrize("golden", ["R1_caustic_rr_64x64_spp16", "R2_hardlight_rr_64x64_spp16",
+                                    "R3_cbox_low_rr_64x64_spp4"])
+def test_adapter_rr_frame_matches_reference_golden(tmp_path, golden_manifest, golden):
+    m = golden_manifest["rr_framebuffers"][golden]
+    W, H, spp, rr = m["width"], m["height"], m["spp"], m["rr_depth"]
+    toml = _toml(tmp_path, m["scene"], W, H, spp, rr)
+    out = tmp_path / "fb.f32"
+    r = subprocess.run([CHECK_RR, "frame", str(toml), str(W), str(H), str(spp), str(out)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    fb = np.fromfile(out, np.float32).reshape(H, W, 3)
+    err = _rel_l2(fb, load_golden(golden))
+    assert err.max() <= TOL, f"max per-pixel rel L2 {err.max():.3g}"
+
+
+@pytest.mark.parametrize("name, W, H, spp, rr, n, stride", [
+    ("caustic", 64, 64, 16, 3, 1500, 37),
+    ("hardlight", 64, 64, 16, 2, 1000, 41),
+    ("cbox_low", 64, 64, 4, 1, 800, 53),
+])
+def test_adapter_rr_render_ray_sampler_equals_reference_integrator(tmp_path, name, W, H, spp, rr, n, stride):
+    """Russian roulette through the reference's own Sampler: every draw past
+    rrDepth, every stored rrProbability; Li, generator state and splats bit for bit."""
+    toml = _toml(tmp_path, name, W, H, spp, rr)
+    r = subprocess.run([CHECK_RR, "samples", str(toml), str(W), str(H), str(spp), str(n), str(stride)],
+                       capture_output=True, text=True, timeout=600)
+    out = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {}
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert out["li_mismatch"] == 0 and out["state_mismatch"] == 0 and out["splat_mismatch"] == 0, out
+    assert out["nonzero_li"] > n // 4

@@ -573,3 +573,74 @@ def test_gpu_single_sample_api_other_integrators(integ):
         ray, sampler = driver_ray(p, name, pixel, k)
         Li = it.render(ray, sampler)
         assert np.allclose(Li, Li_ref, rtol=1e-6, atol=0), (pixel, k, Li, Li_ref)
+
+
+# ---- Russian roulette (the reference's NO_RR = 0 branch, bdpt.h:18, :68, :129-132, :188, :201-204)
+RR_CASES = ["R1_caustic_rr_64x64_spp16", "R2_hardlight_rr_64x64_spp16", "R3_cbox_low_rr_64x64_spp4",
+            "R4_caustic_rr1_48x48_spp4", "R5_hardlight_mirror_rr_48x48_spp4", "R6_caustic_rr_512x512_spp2_rows32"]
+
+
+def rr_integrator(name, W, H, spp, rr, obj=None, cam=None):
+    cam = cam or variants.SCENES[name]["camera"]
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**cam), width=W, height=H, spp=spp, rr_depth=rr,
+                          russian_roulette=bdpt_amd.RR_LUMINANCE)
+    it = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(obj) if obj else scene(name), cfg)
+    it.init()
+    return it
+
+
+@pytest.mark.parametrize("name", RR_CASES)
+def test_gpu_russian_roulette_matches_reference_golden(name, golden_manifest):
+    """The RR build of the megakernel (bdpt_kernels_rr.hip) against the reference
+    compiled with NO_RR = 0 (oracle/_ref/ref_bdpt_rr)."""
+    m = golden_manifest["rr_framebuffers"][name]
+    it = rr_integrator(m["scene"], m["width"], m["height"], m["spp"], m["rr_depth"])
+    fb = it.render_frame(row_offset=0, row_stride=m["row_stride"]).reshape(-1)
+    assert it.stats()["capped_samples"] == 0
+    worst, exact, _ = report(fb, load_golden(name))
+    assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact floats {exact:.4f})"
+
+
+@pytest.mark.parametrize("rr,W,H,spp", [(2, 24, 16, 4), (6, 16, 12, 4), (40, 12, 8, 2)])
+def test_gpu_russian_roulette_closed_box_matches_oracle(rr, W, H, spp, tmp_path):
+    """In the closed box no path escapes: subpaths end only by roulette (p = 0.5
+    once the throughput's luminance is below 0.01), so they run long and draw
+    far past the lazy MT19937 window; same frame as the oracle's NO_RR = 0."""
+    obj = variants.closed_box_obj(str(tmp_path))
+    cam = variants.CLOSED_CAMERA
+    it = rr_integrator(None, W, H, spp, rr, obj=obj, cam=cam)
+    fb = it.render_frame().reshape(-1)
+    assert it.stats()["capped_samples"] == 0
+    O.counters(True)
+    ref, n = O.Scene(obj).render(O.make_params(cam, W, H, spp, rr, 0, russian_roulette=1))
+    c = O.counters(True)
+    assert c["light_verts"] / n > rr - 1  # paths go past rrDepth
+    worst, exact, _ = report(fb, ref.reshape(-1))
+    assert worst <= TOL, f"rr={rr}: max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
+
+
+@pytest.mark.parametrize("pixel,k", [(0, 0), (2080, 3), (1000, 15), (4095, 7), (2500, 9), (1234, 1)])
+def test_gpu_russian_roulette_single_sample_matches_oracle(pixel, k):
+    """render(ray, sampler) with NO_RR = 0: Li and the splat list as the oracle's sample."""
+    W = H = 64
+    spp, rr = 16, 3
+    it = rr_integrator("caustic", W, H, spp, rr)
+    p = O.make_params(variants.SCENES["caustic"]["camera"], W, H, spp, rr, 0, russian_roulette=1)
+    sc = O.Scene(variants.obj_path("caustic"))
+    Li_ref, splats_ref = sc.sample(p, pixel, k)
+    ray, sampler = driver_ray(p, "caustic", pixel, k)
+    Li = it.render(ray, sampler)
+    assert np.allclose(Li, Li_ref, rtol=1e-6, atol=0), (Li, Li_ref)
+    assert rel_l2(it.rgb.reshape(-1), splats_ref).max() <= TOL
+
+
+def test_gpu_russian_roulette_limits():
+    """rrDepth past 192 with roulette is refused (subpaths are bounded at 256
+    vertices); an unknown mode is an error; the default NO_RR image differs."""
+    it = rr_integrator("cbox_low", 8, 8, 1, 193)
+    with pytest.raises(bdpt_amd.BdptError, match="rr_depth"):
+        it.render_frame()
+    it = integrator("cbox_low", 8, 8, 1, 5)
+    it.config.russian_roulette = 7
+    with pytest.raises(bdpt_amd.BdptError, match="russian_roulette"):
+        it.render_frame()

@@ -39,6 +39,33 @@ def test_oracle_framebuffer_bit_exact(name, golden_manifest):
     assert mism.size == 0, f"{mism.size} floats differ, first at {mism[:5]}"
 
 
+RR_CASES = ["R1_caustic_rr_64x64_spp16", "R2_hardlight_rr_64x64_spp16", "R3_cbox_low_rr_64x64_spp4",
+            "R4_caustic_rr1_48x48_spp4", "R5_hardlight_mirror_rr_48x48_spp4", "R6_caustic_rr_512x512_spp2_rows32"]
+
+
+@pytest.mark.parametrize("name", RR_CASES)
+def test_oracle_russian_roulette_bit_exact(name, golden_manifest):
+    """NO_RR = 0 (bdpt.h:18): the reference built with its Russian-roulette
+    branch (oracle/_ref/ref_bdpt_rr) against the oracle's russian_roulette = 1."""
+    meta = golden_manifest["rr_framebuffers"][name]
+    sc = variants.SCENES[meta["scene"]]
+    scene = O.Scene(variants.obj_path(meta["scene"]))
+    p = O.make_params(sc["camera"], meta["width"], meta["height"], meta["spp"], meta["rr_depth"], 0,
+                      russian_roulette=1)
+    rows = list(range(0, meta["height"], meta["row_stride"]))
+    O.lib().tro_rr_overflow(1)
+    fb, n = scene.render(p, rows=rows)
+    assert n == meta["samples"] and O.lib().tro_rr_overflow(1) == 0
+    ref = load_golden(name)
+    assert hashlib.sha256(ref.tobytes()).hexdigest() == meta["sha256"]
+    mism = np.flatnonzero(fb.view(np.uint32) != ref.view(np.uint32))
+    assert mism.size == 0, f"{mism.size} floats differ, first at {mism[:5]}"
+    # the mode matters: NO_RR = 1 gives a different image on every scene
+    p.russian_roulette = 0
+    fb0, _ = scene.render(p, rows=rows)
+    assert not np.array_equal(fb0, ref)
+
+
 @pytest.mark.parametrize("scene_name", ["cbox_low", "caustic", "hardlight", "hardlight_mirror", "synth1m"])
 def test_oracle_scene_ingest_matches_reference(scene_name, golden_manifest):
     meta = golden_manifest["scenes"][scene_name]
