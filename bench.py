@@ -225,7 +225,7 @@ def main() -> None:
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    kernel_ms = []
+    kernel_ms, reduce_ms = [], []
 
     row_offset, row_stride = bdpt_dist.row_shard(rank, world)
 
@@ -236,11 +236,16 @@ def main() -> None:
         kernel_ms.append(st["kernel_ms"])
         if args.integrator == "path":
             integ.check_levels()  # a sample past the 512-level stack would not be the reference's
-        bdpt_dist.reduce_framebuffer(fb, dst=0)
+        if world > 1:  # the exchange step, timed on its own (host wall: it includes waiting for slower ranks)
+            r0 = time.perf_counter()
+            bdpt_dist.reduce_framebuffer(fb, dst=0)
+            torch.cuda.synchronize(dev)
+            reduce_ms.append((time.perf_counter() - r0) * 1e3)
 
     for _ in range(args.warmup):
         step()
     kernel_ms.clear()
+    reduce_ms.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -259,6 +264,20 @@ def main() -> None:
     value = samples_total * args.steps / elapsed * 1e-6
     local_samples = integ.stats()["samples"]
     avg_kernel_ms = sum(kernel_ms) / max(len(kernel_ms), 1)
+    ranks = None
+    if world > 1:
+        # what every rank saw: its render-kernel time, its reduce time, its samples
+        mine = torch.tensor([avg_kernel_ms, sum(reduce_ms) / max(len(reduce_ms), 1), float(local_samples)],
+                            dtype=torch.float64, device="cpu" if rehearsal else dev)
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        per = [v.cpu().tolist() for v in allv]
+        ranks = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                 "rehearsal_one_device": rehearsal,
+                 "kernel_ms": [round(k, 3) for k, _, _ in per], "reduce_ms": [round(r, 3) for _, r, _ in per],
+                 "samples": [int(n) for _, _, n in per],
+                 "kernel_ms_min": round(min(k for k, _, _ in per), 3), "kernel_ms_max": round(max(k for k, _, _ in per), 3),
+                 "reduce_bytes": W * H * 3 * 4}
 
     if rank == 0 and args.integrator in ("path", "direct"):
         metric = ("Msamples/sec, PathTracerIntegrator (path.h, explicit, RR 0.95 past depth 5)"
@@ -271,6 +290,8 @@ def main() -> None:
                "config": {"workload": f"{args.integrator}_{args.scene}_{W}x{H}_{spp}spp",
                           "scene": SCENE_LABEL.get(args.scene),
                           "kernel_ms": round(avg_kernel_ms, 3)}}
+        if ranks:
+            out["ranks"] = ranks
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.scene, W, H, spp, rr, integrator=args.integrator)
         print(json.dumps(out), flush=True)
@@ -332,9 +353,12 @@ def main() -> None:
                      else "synthetic camera samples over a generated 1M-triangle scene"),
             "config": {"workload": f"{args.scene}_{W}x{H}_{spp}spp", "scene": SCENE_LABEL.get(args.scene, args.scene),
                        "width": W, "height": H, "spp": spp, "rr_depth": rr, "samples_per_step": samples_total,
-                       "parallelism": f"{world}-way row-interleaved shards + RCCL sum-reduce"},
+                       "parallelism": (f"{world}-way row-interleaved shards + one framebuffer sum-reduce "
+                                       f"({ranks['backend']})" if ranks else "one GPU, whole image (no reduce)")},
             "roofline": roof,
         }
+        if ranks:
+            out["ranks"] = ranks
         if world == 1 and not args.no_cpu:
             ref_fb = None if args.no_parity else os.path.join("/tmp", f"bench_ref_fb_{os.getpid()}.f32")
             cb = cpu_baseline(args.scene, W, H, spp, rr, frame_out=ref_fb)

@@ -172,3 +172,7 @@ def test_gpu_bench_two_rank_rehearsal(tmp_path):
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["samples_per_step"] == 64 * 64 * 4
+    rk = out["ranks"]  # what a scaling run needs to be diagnosed
+    assert rk["world_size"] == 2 and rk["backend"] == "gloo" and rk["rehearsal_one_device"]
+    assert len(rk["kernel_ms"]) == 2 and min(rk["kernel_ms"]) > 0 and len(rk["reduce_ms"]) == 2
+    assert sum(rk["samples"]) == 64 * 64 * 4 and rk["kernel_ms_max"] >= rk["kernel_ms_min"]
