@@ -1107,10 +1107,17 @@ int bdpt_intersect(bdpt_ctx* c, int64_t n, const float* rays, int32_t occlusion,
     void *dr, *dout;
     const size_t N = static_cast<size_t>(n);
     if ((rc = kat_in(c, kb, rays, 32 * N, &dr)) || (rc = kat_in(c, kb, nullptr, 80 * N, &dout))) return rc;
+    // The interior-box test the frame kernels would use for these origins: without
+    // the ambiguity slack when every origin lies within 100 scene diagonals (as
+    // for a frame whose camera does, node_slack_needed), with it otherwise.
+    std::vector<const float*> origins(N);
+    for (size_t i = 0; i < N; i++) origins[i] = rays + 8 * i;
+    dev::DevScene sc = c->sc;
+    sc.node_slack = node_slack_needed(c, origins.data(), static_cast<int>(std::min<size_t>(N, 0x7fffffff)));
     // the traversal-stack overflow columns serve c->nslots rays at a time
     for (int64_t b = 0; b < n; b += c->nslots) {
         const int64_t m = std::min<int64_t>(c->nslots, n - b);
-        HIP_TRY(launch_intersect_kat(c->sc, m, occlusion ? 1 : 0, static_cast<const float*>(dr) + 8 * b, c->gstack,
+        HIP_TRY(launch_intersect_kat(sc, m, occlusion ? 1 : 0, static_cast<const float*>(dr) + 8 * b, c->gstack,
                                      c->nslots, static_cast<float*>(dout) + 20 * b, c->stream));
     }
     HIP_TRY(hipMemcpyAsync(out, dout, 80 * N, hipMemcpyDeviceToHost, c->stream));

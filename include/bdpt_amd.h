@@ -381,7 +381,10 @@ typedef struct {
 } bdpt_hit;
 /* rays: n x 8 (o.xyz d.xyz min_t max_t). occlusion = 0: closest hit (accel.h:125);
  * 1: the any-hit query of visibilityQuery (bvh.h:259-352 with occlusion = true),
- * result in hit only. */
+ * result in hit only. The traversal is the frame kernels' (culled 4-wide tree,
+ * reference-leaf check), with the interior-box test a frame would use for the
+ * batch's origins: without the ambiguity slack when all lie within 100 scene
+ * diagonals, with it otherwise. */
 int bdpt_intersect(bdpt_ctx* ctx, int64_t n, const float* rays, int32_t occlusion, bdpt_hit* out);
 /* BDPTIntegrator::splatToImagePlane (bdpt.h:485-496) of points p (n x 3) for the
  * camera and image of params: xy = n x 2 (the reference's int truncation). */

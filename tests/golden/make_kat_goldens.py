@@ -11,6 +11,9 @@ of the BDPT path (ref_bdpt kat / sample_state, oracle/ref/ref_driver.cpp):
   kat_triangle.npz          rayTriangleIntersect (core.h:379-400)
   kat_intersect_<scene>.npz AcceleratorBVH::intersect + the any-hit query (accel.h:125-172, bvh.h:259-352)
   kat_splat.npz             BDPTIntegrator::splatToImagePlane (bdpt.h:485-496)
+  kat_adversarial_<scene>.npz  AcceleratorBVH::intersect + the any-hit query on rays where the
+                            product traversal's exactness argument is thinnest (grazing, ties,
+                            surface origins, origins beyond 100 scene diagonals)
   kat_sampler_<integ>.npz   Integrator::render(ray, sampler) from arbitrary std::mt19937 states
                             (integrator.h:31; bdpt.h:219, path.h:235, direct.h:449)
 """
@@ -173,6 +176,130 @@ def intersect_fixture(scene, n, seed):
     print("intersect", scene, n, "hits", int(out[:, 0].sum()), "occluded", int(out[:, 20].sum()))
 
 
+def _normalize(v):
+    return (v / np.linalg.norm(v, axis=-1, keepdims=True)).astype(f32)
+
+
+def _surface_points(rng, tri, idx):
+    """Points on triangles idx as the path computes hit points (shade_hit /
+    SurfaceInteraction: (v0 w + v1 u) + v2 v in float32), with a share exactly on
+    edges and vertices."""
+    n = idx.size
+    u = rng.random(n).astype(f32)
+    v = (rng.random(n) * (1 - u)).astype(f32)
+    k = rng.random(n)
+    u[k < 0.1] = 0
+    v[(k >= 0.1) & (k < 0.2)] = 0
+    e = (k >= 0.2) & (k < 0.3)
+    v[e] = (f32(1) - u[e]).astype(f32)
+    c = (k >= 0.3) & (k < 0.35)
+    u[c], v[c] = 0, 0
+    w = (f32(1) - u - v).astype(f32)
+    v0, v1, v2 = tri[idx, 0:3], tri[idx, 3:6], tri[idx, 6:9]
+    return ((v0 * w[:, None] + v1 * u[:, None]) + v2 * v[:, None]).astype(f32)
+
+
+def adversarial_rays(scene, n, seed):
+    """Rays chosen where the product traversal's exactness argument is thinnest
+    (DESIGN.md §2 items 5-6): the computed hit of Moller-Trumbore near |det| = 1e-8,
+    ties between triangles sharing an edge or a vertex, origins on surfaces, and
+    origins beyond 100 scene diagonals. Returns (rays [n, 8] float32, kind [n])."""
+    sys.path.insert(0, os.path.join(REPO, "bidirectional-path-tracing_amd"))
+    import bdpt_amd
+
+    rng = np.random.default_rng(seed)
+    tf, ti, nf, _ = bdpt_amd.Scene(variants.obj_path(scene)).export()
+    tri = tf[:, :9].astype(f32)
+    e1, e2 = tri[:, 3:6] - tri[:, 0:3], tri[:, 6:9] - tri[:, 0:3]
+    cr = np.cross(e1.astype(np.float64), e2.astype(np.float64))
+    area = 0.5 * np.linalg.norm(cr, axis=1)
+    ok = area > 0
+    ng = np.zeros_like(cr)
+    ng[ok] = cr[ok] / np.linalg.norm(cr[ok], axis=1, keepdims=True)
+    lo, hi = nf[0, :3].astype(np.float64), nf[0, 3:].astype(np.float64)
+    diag = float(np.linalg.norm(hi - lo))
+    centre = (lo + hi) / 2
+    big = np.argsort(-area)[:64]  # walls, floor, ceiling, box faces, light
+    shapes, counts = np.unique(ti[:, 0], return_counts=True)
+    curved = np.flatnonzero(ti[:, 0] == shapes[np.argmax(counts)])  # the tessellated sphere(s)
+    FLT_MAX = 3.402823466e38
+    k = n // 6
+    out, kind = [], []
+
+    def add(o, d, mn, mx, tag):
+        m = o.shape[0]
+        out.append(np.concatenate([o, _normalize(d), np.broadcast_to(np.float32(mn), (m, 1)) if np.isscalar(mn)
+                                   else mn[:, None], np.broadcast_to(np.float32(mx), (m, 1)) if np.isscalar(mx)
+                                   else mx[:, None]], 1).astype(f32))
+        kind.append(np.full(m, tag, np.int32))
+
+    # 0: grazing continuation rays from points on the large triangles, |sin| from 0 to 1e-2
+    idx = rng.choice(big, k)
+    o = _surface_points(rng, tri, idx)
+    t1 = _normalize(e1[idx])
+    t2 = _normalize(np.cross(ng[idx], t1))
+    phi = rng.random(k) * 2 * np.pi
+    delta = rng.choice([0.0, 1e-9, 3e-9, 1e-8, 3e-8, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2], k) * rng.choice([-1, 1], k)
+    d = t1 * np.cos(phi)[:, None] + t2 * np.sin(phi)[:, None] + ng[idx] * delta[:, None]
+    h = rng.choice([0.0, 0.0, 1e-7, -1e-7, 1e-6, -1e-6, 1e-5, 1e-4], k)
+    add((o + ng[idx] * h[:, None]).astype(f32), d, 1e-8, FLT_MAX, 0)
+    # 1: grazing shadow segments between two points of the same large triangle (visibilityQuery)
+    idx = rng.choice(big, k)
+    a, b = _surface_points(rng, tri, idx), _surface_points(rng, tri, idx)
+    lift = rng.choice([0.0, 1e-7, 1e-5, 1e-3], k)[:, None] * ng[idx]
+    a, b = (a + lift).astype(f32), (b + lift).astype(f32)
+    dd = (b - a).astype(f32)
+    dist = np.sqrt((dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1]) + dd[:, 2] * dd[:, 2]).astype(f32)
+    keep = dist > 1e-4
+    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 1)
+    # 2: rays through the curved mesh's vertices and edges (ties between neighbours, silhouettes)
+    idx = rng.choice(curved, k)
+    w = rng.choice(4, k)
+    tgt = np.where((w == 0)[:, None], tri[idx, 0:3], np.where((w == 1)[:, None], (tri[idx, 0:3] + tri[idx, 3:6]) / 2,
+                   _surface_points(rng, tri, idx)))
+    eye = np.array(variants.SCENES[scene]["camera"]["eye"], np.float64)
+    inner = lo + rng.random((k, 3)) * (hi - lo)
+    o = np.where((rng.random(k) < 0.5)[:, None], eye, inner).astype(f32)
+    add(o, tgt - o, 1e-8, FLT_MAX, 2)
+    # 3: continuation rays from surface points of any triangle, both hemispheres, near-tangent included
+    idx = rng.integers(0, tri.shape[0], k)
+    o = _surface_points(rng, tri, idx)
+    d = rng.normal(size=(k, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    flat = rng.random(k) < 0.3
+    d[flat] -= ng[idx][flat] * np.sum(d[flat] * ng[idx][flat], 1, keepdims=True) * (1 - rng.choice(
+        [1e-6, 1e-4, 1e-2], flat.sum()))[:, None]
+    add(o, d, 1e-8, FLT_MAX, 3)
+    # 4: origins 100 - 10000 scene diagonals away, aimed at surface points (the slack-test regime)
+    dirn = rng.normal(size=(k, 3))
+    dirn /= np.linalg.norm(dirn, axis=1, keepdims=True)
+    far = diag * np.exp(rng.uniform(np.log(100.0), np.log(10000.0), k))
+    o = (centre + dirn * far[:, None]).astype(f32)
+    tgt = _surface_points(rng, tri, rng.integers(0, tri.shape[0], k))
+    mx = np.where(rng.random(k) < 0.5, FLT_MAX, far * 1.5).astype(f32)
+    add(o, tgt - o, np.where(rng.random(k) < 0.5, 1.0, 1e-8).astype(f32), mx, 4)
+    # 5: shadow segments between surface points of any two triangles
+    m = n - 5 * k
+    a = _surface_points(rng, tri, rng.integers(0, tri.shape[0], m))
+    b = _surface_points(rng, tri, rng.integers(0, tri.shape[0], m))
+    dd = (b - a).astype(f32)
+    dist = np.sqrt((dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1]) + dd[:, 2] * dd[:, 2]).astype(f32)
+    keep = dist > 1e-4
+    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 5)
+    return np.concatenate(out), np.concatenate(kind)
+
+
+def adversarial_fixture(scene, n, seed):
+    rays, kind = adversarial_rays(scene, n, seed)
+    out = kat(toml(scene), 64, 64, "intersect", rays, 21)
+    np.savez_compressed(os.path.join(HERE, f"kat_adversarial_{scene}.npz"), rays=rays, kind=kind,
+                        hit=out[:, 0].astype(np.int8), t=out[:, 1], u=out[:, 2], v=out[:, 3],
+                        shape=out[:, 4].view(np.int32), prim=out[:, 5].view(np.int32),
+                        occluded=out[:, 20].astype(np.int8))
+    print("adversarial", scene, rays.shape[0], "rays; hits", int(out[:, 0].sum()), "occluded",
+          int(out[:, 20].sum()), "per kind", np.bincount(kind))
+
+
 def splat_fixture(seed=5):
     rng = np.random.default_rng(seed)
     res = {}
@@ -226,6 +353,10 @@ def sampler_fixture(name, scene, toml_path, W, H, spp, rr, n, seed):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "adversarial":  # only these fixtures
+        for i, (sc, n) in enumerate([("caustic", 48000), ("hardlight", 48000), ("synth1m", 30000)]):
+            adversarial_fixture(sc, n, seed=40 + i)
+        return
     if not os.path.exists(REF):
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle", "ref")], check=True)
     for i, sc in enumerate(["caustic", "hardlight", "hardlight_mirror", "hardlight_phong", "cbox_low"]):
@@ -235,6 +366,8 @@ def main():
     for i, (sc, n) in enumerate([("caustic", 12000), ("hardlight", 8000), ("cbox_low", 4000)]):
         intersect_fixture(sc, n, seed=20 + i)
     splat_fixture()
+    for i, (sc, n) in enumerate([("caustic", 48000), ("hardlight", 48000), ("synth1m", 30000)]):
+        adversarial_fixture(sc, n, seed=40 + i)
     sampler_fixture("bdpt_caustic", "caustic", toml("caustic", 64, 64, 16, 8), 64, 64, 16, 8, 160, 30)
     sampler_fixture("bdpt_hardlight_rr12", "hardlight", toml("hardlight", 64, 64, 16, 12), 64, 64, 16, 12, 100, 31)
     sampler_fixture("path_caustic", "caustic", toml("caustic", 64, 64, 16, kind="path"), 64, 64, 16, 5, 80, 32)

@@ -110,6 +110,35 @@ def test_gpu_intersect_matches_reference(scene):
     assert np.array_equal(occ["hit"], ref[:, 20].astype(np.int32))
 
 
+@pytest.mark.parametrize("scene", ["caustic", "hardlight", "synth1m"])
+def test_gpu_intersect_adversarial_rays_match_reference(scene):
+    """Where the traversal's exactness argument is thinnest (DESIGN.md §2 items
+    5-6; tests/golden/make_kat_goldens.py adversarial_rays): grazing continuation
+    rays and shadow segments along the large triangles (|det| down to 1e-8),
+    rays through the curved mesh's shared vertices and edges (ties), rays
+    starting on surfaces, and origins 100 - 10000 scene diagonals away. Closest
+    hit (acceptance, t, u, v, shape, prim) and occlusion bit for bit against the
+    reference's AcceleratorBVH; the in-scene batches run the frames' slack-free
+    interior test, the far batch and the mixed batch the slack test."""
+    g = kat(f"kat_adversarial_{scene}")
+    it = integrator(scene)
+    rays, kind = g["rays"], g["kind"]
+    far = kind == 4
+    for sel in (~far, far, np.ones_like(far)):
+        h = it.intersect(rays[sel])
+        hit = g["hit"][sel].astype(np.int32)
+        bad = np.flatnonzero(h["hit"] != hit)
+        assert bad.size == 0, f"{bad.size} acceptance mismatches, kinds {np.bincount(kind[sel][bad])}"
+        k = hit == 1
+        assert same_bits(h["t"][k], g["t"][sel][k]) and same_bits(h["u"][k], g["u"][sel][k])
+        assert same_bits(h["v"][k], g["v"][sel][k])
+        assert np.array_equal(h["shape_id"][k], g["shape"][sel][k]) and np.array_equal(h["prim_id"][k],
+                                                                                          g["prim"][sel][k])
+        occ = it.intersect(rays[sel], occlusion=True)
+        bad = np.flatnonzero(occ["hit"] != g["occluded"][sel].astype(np.int32))
+        assert bad.size == 0, f"{bad.size} occlusion mismatches, kinds {np.bincount(kind[sel][bad])}"
+
+
 def test_gpu_splat_to_image_plane_matches_reference():
     """splatToImagePlane (bdpt.h:485-496), incl. points behind the camera and off
     the image (the reference's int truncation)."""

@@ -70,14 +70,39 @@ def test_gpu_matches_reference_golden(name, golden_manifest):
     assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact floats {exact:.4f}, image {whole:.3g})"
 
 
-def test_gpu_full_traversal_equals_culled_traversal():
+@pytest.mark.parametrize("name,W,H,spp,rr", [("caustic", 64, 64, 16, 8), ("hardlight", 64, 64, 16, 2),
+                                             ("hardlight_mirror", 48, 48, 8, 5), ("synth1m", 32, 24, 2, 8)])
+def test_gpu_full_traversal_equals_culled_traversal(name, W, H, spp, rr):
     """The reference's own binary tree walked without culling (FULL) and the
     4-wide hierarchy with distance culling give the same closest hits."""
-    a = integrator("caustic", 64, 64, 16, 8)
+    a = integrator(name, W, H, spp, rr)
     fa = a.render_frame().copy()
-    b = integrator("caustic", 64, 64, 16, 8)
+    b = integrator(name, W, H, spp, rr)
     fb = b.render_frame(flags=bdpt_amd.FLAG_FULL_TRAVERSAL).copy()
     assert rel_l2(fa, fb).max() <= TOL
+
+
+# beyond 100 diagonals (the slack decision) and within the camera ray's max_t of 1000 (renderer.cpp:192)
+@pytest.mark.parametrize("name,dist", [("caustic", 150.0), ("hardlight", 250.0), ("caustic", 280.0)])
+def test_gpu_far_camera_takes_the_slack_test_and_matches_oracle(name, dist):
+    """A camera more than 100 scene diagonals away: the host keeps the interior
+    boxes' ambiguity slack (node_slack_needed) and the frame
+    still equals the oracle's (a narrow field of view keeps the box in view)."""
+    cam = dict(variants.SCENES[name]["camera"])
+    eye, at = np.array(cam["eye"], np.float64), np.array(cam["at"], np.float64)
+    fwd = (at - eye) / np.linalg.norm(at - eye)
+    diag = 2.0 * np.sqrt(3.0)  # ~ the Cornell boxes' diagonal
+    cam["eye"] = list(at - fwd * dist * diag)
+    cam["fov"] = float(np.degrees(2 * np.arctan(1.2 / (dist * diag))))
+    W, H, spp, rr = 32, 32, 4, variants.SCENES[name]["rr_depth"]
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**cam), width=W, height=H, spp=spp, rr_depth=rr)
+    it = bdpt_amd.BDPTIntegrator(scene(name), cfg)
+    it.init()
+    fb = it.render_frame().reshape(-1)
+    ref, _ = O.Scene(variants.obj_path(name)).render(O.make_params(cam, W, H, spp, rr))
+    assert (ref.reshape(-1, 3).sum(1) > 0).mean() > 0.2  # the box is in view
+    worst, exact, _ = report(fb, ref)
+    assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
 
 
 @pytest.mark.parametrize("name,W,H,spp,rr", [
