@@ -83,12 +83,15 @@ int fail(int code, const std::string& msg) {
 
 constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
 constexpr int kMaxRrDepth = 1024;  // beyond 28 the megakernel continues MT19937 from an HBM ring
-// Russian roulette (NO_RR = 0): subpaths are unbounded in the reference; here a
-// subpath that reaches this depth ends and the sample is counted as capped (the
-// render then fails rather than return a different image). The light-vertex
-// store holds kRrDepthCap - 1 vertices per lane slot (64 B each).
-constexpr int kRrDepthCap = 256;
-constexpr int kRrMaxRrDepth = 192;
+// Russian roulette (NO_RR = 0): subpaths are unbounded in the reference (a light
+// subpath trapped by total internal reflection in the Caustic sphere was measured
+// at 67 714 bounces). Here the light-vertex store of a lane slot holds
+// max(kRrLightVerts, rrDepth - 1) vertices (64 B each; the shipped scenes store at
+// most 36), and a walk past kRrDepthGuard bounces is a hang guard; a sample that
+// meets either is counted (bdpt_stats.capped_samples) and the host render fails
+// rather than return a different image.
+constexpr int kRrLightVerts = 255;
+constexpr int kRrDepthGuard = 1 << 20;
 }  // namespace
 
 // Error reporting shared with the other C-ABI translation units (exr_io.cpp, toml_config.cpp).
@@ -145,7 +148,7 @@ struct bdpt_ctx {
     size_t pt_levels_f4 = 0;
     uint32_t* pt_ring = nullptr;
     uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28, RR)
-    uint32_t* capped = nullptr;   // samples that reached kRrDepthCap (Russian roulette), per call
+    uint32_t* capped = nullptr;   // samples that met the Russian-roulette bounds, per call
     void* pt_dparams = nullptr;
     // single-sample calls: the caller's std::mt19937 state and the splat list
     uint32_t* mt_state = nullptr;  // BDPT_MT19937_WORDS
@@ -466,9 +469,6 @@ static int check_params(const bdpt_frame_params* p) {
     if (p->row_stride < 1 || p->row_offset < 0) return fail(BDPT_ERR_INVALID, "bad row shard");
     if (p->russian_roulette != BDPT_RR_NONE && p->russian_roulette != BDPT_RR_LUMINANCE)
         return fail(BDPT_ERR_INVALID, "unknown russian_roulette mode");
-    if (p->russian_roulette == BDPT_RR_LUMINANCE && p->rr_depth > kRrMaxRrDepth)
-        return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 192 with Russian roulette (subpaths are bounded at 256 "
-                                          "vertices) is not supported");
     return BDPT_OK;
 }
 
@@ -483,13 +483,14 @@ static dev::DevFrame make_frame(const bdpt_frame_params* p) {
     fr.flags = p->flags;
     fr.total_samples = static_cast<uint64_t>(fr.nrows) * static_cast<uint64_t>(p->width) * p->spp;
     fr.rr_mode = p->russian_roulette == BDPT_RR_LUMINANCE ? 1 : 0;
-    fr.depth_cap = fr.rr_mode ? kRrDepthCap : p->rr_depth;
+    fr.depth_cap = fr.rr_mode ? kRrDepthGuard : p->rr_depth;
+    fr.lv_max = fr.rr_mode ? std::max(kRrLightVerts, p->rr_depth - 1) : std::max(p->rr_depth - 1, 1);
     fr.capped = nullptr;  // the context's word, set by the caller
     return fr;
 }
 
-static int ensure_lv(bdpt_ctx* c, int depth_bound, uint32_t nslots) {
-    const size_t need = static_cast<size_t>(std::max(depth_bound - 1, 1)) * light_vertex_fields() * nslots;
+static int ensure_lv(bdpt_ctx* c, int lv_max, uint32_t nslots) {
+    const size_t need = static_cast<size_t>(std::max(lv_max, 1)) * light_vertex_fields() * nslots;
     if (need > c->lv_floats) {
         if (c->lv) HIP_TRY(hipFree(c->lv));
         c->lv = nullptr;
@@ -539,7 +540,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     if (hbm && (p->rr_depth > kLazyRrDepth || rr))
         return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 or Russian roulette with BSDF records in HBM (too many "
                                           "materials for the LDS table) is not built");
-    if ((rc = ensure_lv(c, fr.depth_cap, c->nslots))) return rc;
+    if ((rc = ensure_lv(c, fr.lv_max, c->nslots))) return rc;
     dev::DevScene sc = c->sc;
     sc.node_slack = node_slack_needed(c, eye, 1);
     if (p->rr_depth > kLazyRrDepth || rr) {  // draws past 226: the lanes' MT19937 rings
@@ -917,8 +918,8 @@ int bdpt_render_host(bdpt_ctx* c, const bdpt_frame_params* p, float* fb_host) {
         if ((rc = bdpt_get_stats(c, &st))) return rc;
         if (st.capped_samples)
             return fail(BDPT_ERR_UNSUPPORTED, std::to_string(st.capped_samples) +
-                                                  " samples had a subpath reach the 256-vertex bound of Russian "
-                                                  "roulette; the image is not the reference's");
+                                                  " samples met the Russian-roulette bounds (light-vertex store / "
+                                                  "bounce guard); the image is not the reference's");
     }
     return BDPT_OK;
 }
@@ -931,7 +932,7 @@ static int render_bdpt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const flo
     if (rc) return rc;
     if ((rc = check_mt_state(state))) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    if ((rc = ensure_lv(c, p->russian_roulette ? kRrDepthCap : p->rr_depth, c->nslots))) return rc;
+    if ((rc = ensure_lv(c, make_frame(p).lv_max, c->nslots))) return rc;
     // a sample splats at most once per light vertex: rr_depth bounds the list
     // without Russian roulette; with it the list grows on demand (below)
     if ((rc = ensure_sample_buffers(c, std::max(p->rr_depth, 1)))) return rc;
@@ -964,7 +965,8 @@ static int render_bdpt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const flo
         if ((rc = end_use(c, c->stream))) return rc;
         HIP_TRY(hipStreamSynchronize(c->stream));
         if (capped)
-            return fail(BDPT_ERR_UNSUPPORTED, "a subpath reached the 256-vertex bound of Russian roulette");
+            return fail(BDPT_ERR_UNSUPPORTED, "the sample met the Russian-roulette bounds (light-vertex store / "
+                                              "bounce guard)");
         std::memcpy(&n, &list[0], 4);
         if (n <= static_cast<uint32_t>(c->splat_cap)) break;
         // more splats than the device list holds (the kernel counts them all):

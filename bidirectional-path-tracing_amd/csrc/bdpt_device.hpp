@@ -145,8 +145,9 @@ struct DevFrame {
     uint32_t flags;
     uint64_t total_samples;  // nrows * W * spp
     int32_t rr_mode;    // 1: NO_RR = 0 (Russian roulette past rr_depth; the bdpt_kernels_rr.hip build)
-    int32_t depth_cap;  // subpath depth bound: rr_depth under NO_RR; the light-vertex store's bound with RR
-    uint32_t* capped;   // samples whose subpath reached depth_cap with RR on (then not the reference's)
+    int32_t depth_cap;  // subpath depth bound: rr_depth under NO_RR; with RR a guard (2^20 bounces)
+    int32_t lv_max;     // light vertices a lane slot stores: rr_depth - 1 under NO_RR, more with RR
+    uint32_t* capped;   // RR: samples that hit depth_cap or lv_max (the frame is then not the reference's)
 };
 
 struct Ray {
@@ -432,6 +433,16 @@ __device__ __forceinline__ void make_frame(f3 a, f3& s, f3& t) {
 #endif
     s = cross(t, a);
 }
+// The t axis of Frame(a) alone (the part that costs a square root and a
+// reciprocal); s = cross(t, a) is recomputed from it bit for bit (local_with).
+__device__ __forceinline__ f3 frame_t(f3 a) {
+    if (fabsf(a.x) > fabsf(a.y)) {
+        const float inv = rcp_cr(sqrt_cr(a.x * a.x + a.z * a.z));
+        return mk(a.z * inv, 0.f, -a.x * inv);
+    }
+    const float inv = rcp_cr(sqrt_cr(a.y * a.y + a.z * a.z));
+    return mk(0.f, a.z * inv, -a.y * inv);
+}
 __device__ __forceinline__ f3 to_local(f3 s, f3 t, f3 n, f3 v) { return mk(dot(v, s), dot(v, t), dot(v, n)); }
 __device__ __forceinline__ f3 to_world(f3 s, f3 t, f3 n, f3 v) { return (s * v.x + t * v.y) + n * v.z; }
 __device__ __forceinline__ f3 reflect_z(f3 d) { return mk(-d.x, -d.y, d.z); }
@@ -442,6 +453,9 @@ __device__ __forceinline__ f3 local_at(f3 n, f3 v) {
     make_frame(n, s, t);
     return to_local(s, t, n, v);
 }
+// The same with the frame's t axis already known (frame_t(n)).
+__device__ __forceinline__ f3 local_with(f3 t, f3 n, f3 v) { return to_local(cross(t, n), t, n, v); }
+__device__ __forceinline__ f3 world_with(f3 t, f3 n, f3 v) { return to_world(cross(t, n), t, n, v); }
 __device__ __forceinline__ f3 world_at(f3 n, f3 v) {
     f3 s, t;
     make_frame(n, s, t);

@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     const Stack stk{stack_mem + threadIdx.x, kBlock, kLdsStack, kp.gstack, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
-    const LightStore ls = light_store(kp.lv, kp.fr.depth_cap, blockIdx.x * kBlock + threadIdx.x);
+    const LightStore ls = light_store(kp.lv, kp.fr.lv_max, blockIdx.x * kBlock + threadIdx.x);
     unsigned long long* const work = kp.work;
     const uint64_t total = kp.fr.total_samples;
     __shared__ LaneCold cold_mem[kBlock];
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(64) void bdpt_sample_kernel(DevScene sc, DevFrame f
     scene_tables_to_lds(sc);
     if (threadIdx.x != 0) return;
     Counts cnt;
-    const LightStore ls = light_store(lvbuf, fr.depth_cap, 0);
+    const LightStore ls = light_store(lvbuf, fr.lv_max, 0);
     __shared__ LaneCold cold_mem[1];
     Lane L(cold_mem[0]);
     L.rng = LazyMT{0u, 0u, 0u, 0u};  // unused: next1 draws from the caller's state

@@ -116,7 +116,7 @@ typedef struct {
 #define BDPT_RR_NONE 0      /* NO_RR 1: every subpath stops at rrDepth (one draw at the cap) */
 #define BDPT_RR_LUMINANCE 1 /* NO_RR 0: past rrDepth a subpath continues while sampler.next() < rr, with
                                rr = (luminance(throughput) < 0.01 ? 0.5 : 1) stored per vertex and entering
-                               every pdf (rr * pdf); no depth cap */
+                               every pdf (rr * pdf); no depth cap (see bdpt_stats.capped_samples) */
 
 #define BDPT_NUM_COUNTERS 32
 /* counters: [0] closest-hit rays, [1] shadow rays, [2] interior-node visits,
@@ -137,9 +137,10 @@ typedef struct {
     int64_t samples;       /* camera samples rendered by the last call */
     int64_t launches;      /* kernel launches of the last call */
     int64_t counters[BDPT_NUM_COUNTERS];
-    int64_t capped_samples; /* Russian roulette: samples of the last call with a subpath that reached the
-                               256-vertex bound (the reference would have continued; > 0 means the frame
-                               is not the reference's, and bdpt_render_host fails) */
+    int64_t capped_samples; /* Russian roulette: samples of the last call that met a bound the reference
+                               does not have - more than max(255, rr_depth - 1) stored light vertices, or
+                               2^20 bounces in one subpath (> 0 means the frame is not the reference's,
+                               and bdpt_render_host fails) */
 } bdpt_stats;
 
 const char* bdpt_last_error(void);

@@ -99,6 +99,7 @@ def lib():
         L.tro_counters.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
         L.tro_rr_overflow.restype = ctypes.c_int64
         L.tro_rr_overflow.argtypes = [ctypes.c_int]
+        L.tro_walk_stats.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
         L.tro_mt19937_nth.restype = ctypes.c_uint32
         L.tro_mt19937_nth.argtypes = [ctypes.c_uint32, ctypes.c_int]
         L.tro_sampler_nth.restype = ctypes.c_float
@@ -199,6 +200,13 @@ def camera(p: Params) -> np.ndarray:
     out = np.zeros(72, np.float32)
     lib().tro_camera(ctypes.byref(p), out.ctypes.data)
     return out
+
+
+def walk_stats(reset: bool = True) -> dict:
+    """Deepest light / eye subpath and most stored light vertices of one sample (this thread)."""
+    out = (ctypes.c_int64 * 3)()
+    lib().tro_walk_stats(out, 1 if reset else 0)
+    return dict(zip(["max_light_depth", "max_eye_depth", "max_light_verts"], list(out)))
 
 
 def counters(reset: bool = True) -> dict:

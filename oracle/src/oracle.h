@@ -85,6 +85,9 @@ void tro_counters(int64_t out[8], int reset);
 /* Light vertices dropped because a subpath outgrew the oracle's 1024-vertex
  * store (Russian roulette only; always 0 in practice). */
 int64_t tro_rr_overflow(int reset);
+/* Deepest light / eye subpath (depth when its walk ended) and most stored light
+ * vertices of one sample since the last reset, on this thread. */
+void tro_walk_stats(int64_t out[3], int reset);
 
 /* Unit-level hooks for KAT tests. */
 uint32_t tro_mt19937_nth(uint32_t seed, int n);   /* n-th raw output */

@@ -675,7 +675,7 @@ static int continue_walk(const ctx_t* c, hit_t* h, tr_sampler* smp, float rrp, p
 
 #define MAX_LIGHT_VERTS 1024 /* light vertices kept per sample (the reference's vector is unbounded;
                                  a longer subpath is counted in g_ctr[7]'s overflow twin below) */
-static __thread int64_t g_rr_overflow;
+static __thread int64_t g_rr_overflow, g_max_light_depth, g_max_eye_depth, g_max_nl;
 
 /* rrProbability (bdpt.h:127-132 / :199-204): 1 before rrDepth, then 0.5 when the
  * throughput's luminance (getLuminance, math.h:56-58: a glm dot) is below 0.01;
@@ -698,6 +698,11 @@ int64_t tro_rr_overflow(int reset) {
     int64_t v = g_rr_overflow;
     if (reset) g_rr_overflow = 0;
     return v;
+}
+
+void tro_walk_stats(int64_t out[3], int reset) {
+    out[0] = g_max_light_depth, out[1] = g_max_eye_depth, out[2] = g_max_nl;
+    if (reset) g_max_light_depth = g_max_eye_depth = g_max_nl = 0;
 }
 
 /* lightSubpathWalk (bdpt.h:158-217) */
@@ -742,6 +747,8 @@ static int light_walk(const ctx_t* c, tr_sampler* smp, pvert_t* lverts) {
             }
         }
     }
+    if (depth > g_max_light_depth) g_max_light_depth = depth;
+    if (nl > g_max_nl) g_max_nl = nl;
     return nl;
 }
 
@@ -801,6 +808,7 @@ static v3 eye_walk(const ctx_t* c, const pvert_t* lverts, int nl, ray_t ray, tr_
         }
         if (!continue_walk(c, &hit, smp, rrp, &ev, &throughput, &depth, &vc, &vcm, &wi)) break;
     }
+    if (depth > g_max_eye_depth) g_max_eye_depth = depth;
     return Li;
 }
 
