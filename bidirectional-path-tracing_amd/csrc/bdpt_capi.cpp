@@ -392,6 +392,16 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     c->sc.node_slack = 1u;  // per render: node_slack_needed
     c->tri_tree = L.tri_tree;
     for (int a = 0; a < 3; a++) c->box_lo[a] = s->host.nodes[0].bmin[a], c->box_hi[a] = s->host.nodes[0].bmax[a];
+    {  // the region whose queries the culled, padded traversal tree serves (DevScene::near_lo/hi)
+        double diag2 = 0.0;
+        for (int a = 0; a < 3; a++) diag2 += (c->box_hi[a] - c->box_lo[a]) * (c->box_hi[a] - c->box_lo[a]);
+        const double grow = 100.0 * std::sqrt(diag2);
+        for (int a = 0; a < 3; a++) {
+            const double lo = c->box_lo[a] - grow, hi = c->box_hi[a] + grow;
+            c->sc.near_lo[a] = std::isfinite(lo) ? static_cast<float>(lo) : -__builtin_inff();
+            c->sc.near_hi[a] = std::isfinite(hi) ? static_cast<float>(hi) : __builtin_inff();
+        }
+    }
     c->sc.mt_ring = nullptr;
     c->sc.mt_ring_stride = 0;
     c->sc.nemit = static_cast<int32_t>(L.emitters.size());

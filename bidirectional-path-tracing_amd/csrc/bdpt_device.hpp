@@ -67,6 +67,12 @@ struct DevScene {
     // of lane slot s at mt_ring[k * mt_ring_stride + s]; null otherwise
     uint32_t* mt_ring;
     uint32_t mt_ring_stride;
+    // The scene box grown by 100 scene diagonals: a query whose origin lies
+    // outside (far_origin) walks the reference's own binary tree unculled. Far
+    // from the scene Moller-Trumbore's arithmetic loses the hit point (cancellation
+    // in o - v0), so the reference can accept a triangle the ray's line misses by
+    // more than the traversal tree's padding.
+    float near_lo[3], near_hi[3];
 };
 constexpr uint32_t kNoLds = 0xffffffffu;
 constexpr uint32_t kLdsHdr = 4;  // LDS header words: mt_ring (2 words), mt_ring_stride, unused
@@ -493,13 +499,32 @@ __device__ __forceinline__ bool slab(float lx, float ly, float lz, float hx, flo
 // hit / miss outcome is always the reference's. Rays whose reciprocal
 // direction or origin is not finite (where 0 * inf = NaN could arise) take
 // slab() for every box (RayInv::fast == false).
+#ifndef BDPT_CULL_NEAR
+#define BDPT_CULL_NEAR 1  // 0: no box is culled for lying before t = 5e-4 (only the far cull remains)
+#endif
+constexpr float kCullNear = BDPT_CULL_NEAR ? 5e-4f : -__builtin_huge_valf();
+// The near cull assumes Moller-Trumbore puts a hit where the ray meets its
+// triangle. For a ray nearly parallel to a triangle's plane whose origin lies on
+// that plane (a grazing ray leaving a surface) the computed t, u, v are rounding
+// noise the reference still accepts (t > 1e-3), so such queries walk without the
+// near cull: every query leaving a surface at |cos| < kGrazeCos to its shading
+// normal, and the first light-subpath ray.
+constexpr float kGrazeCos = 0.1f;
 enum : int { kSlabMiss = 0, kSlabHit = 1, kSlabAmbiguous = 2 };
 struct RayInv {
     f3 inv;
     bool fast;
+    float near;  // boxes left before t = near are culled (kCullNear, or -inf: no near cull, see cull_near_for)
 };
-__device__ __forceinline__ RayInv ray_inv(const Ray& r) {
+__device__ __forceinline__ bool far_origin(const DevScene& sc, f3 o) {
+    return !(o.x >= sc.near_lo[0] && o.x <= sc.near_hi[0] && o.y >= sc.near_lo[1] && o.y <= sc.near_hi[1] &&
+             o.z >= sc.near_lo[2] && o.z <= sc.near_hi[2]);
+}
+constexpr float kNoCullNear = -__builtin_huge_valf();
+__device__ __forceinline__ RayInv ray_inv(const Ray& r, float near);
+__device__ __forceinline__ RayInv ray_inv(const Ray& r, float near) {
     RayInv ri;
+    ri.near = near;
     ri.inv = mk(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
     const float probe = (ri.inv.x + ri.inv.y + ri.inv.z) * 0.f + ((r.o.x + r.o.y + r.o.z) * 0.f);
     ri.fast = (probe == 0.f);  // false iff some component is +-inf or NaN
@@ -624,7 +649,6 @@ struct LinkStack {
 // entered beyond best + margin, or exited before t = 5e-4, cannot hold a
 // triangle that changes that result.
 __device__ __forceinline__ float cull_far(float best) { return best + fabsf(best) * 1e-3f + 1e-4f; }
-constexpr float kCullNear = 5e-4f;
 
 struct Counts {
     uint32_t c[kCounters];
@@ -895,7 +919,7 @@ __device__ __forceinline__ bool trav_node_vals(float4 lx, float4 hx, float4 ly, 
         float tn, tf;
         const int d = slab_fast(clx, cly, clz, chx, chy, chz, r.o, ri.inv, tn, tf);
         const bool pass = SLACK ? d != kSlabMiss : !(tn > tf);
-        const bool hit = l != kEmptyLinkDev && pass && !(tn > far) && !(tf < kCullNear);
+        const bool hit = l != kEmptyLinkDev && pass && !(tn > far) && !(tf < ri.near);
         key[c] = hit ? tn : __builtin_inff();
         lnk[c] = hit ? l : kEmptyLinkDev;
     }
@@ -1016,11 +1040,11 @@ __device__ __forceinline__ void trav_while_while(const TravScene& sc, const Ray&
 
 template <bool FULL, bool COUNT>
 __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool any, const Stack& stk, float& bt,
-                                        float& bu, float& bv, Counts& cnt) {
+                                        float& bu, float& bv, Counts& cnt, float near = kNoCullNear) {
     if (r.min_t > r.max_t) return -1;  // the root's entry mint is min_t (bvh.h:277, :287)
-    const RayInv ri = ray_inv(r);
-    if (FULL || !ri.fast) {
-        const TravResult q = traverse_binary<COUNT, Stack>(sc, r, any, !FULL, stk);
+    const RayInv ri = ray_inv(r, near);
+    if (FULL || !ri.fast || far_origin(sc, r.o)) {  // the reference's tree, unculled
+        const TravResult q = traverse_binary<COUNT, Stack>(sc, r, any, false, stk);
         if (COUNT) cnt.c[2] += q.nodes, cnt.c[3] += q.tris, cnt.c[15] += q.exact;
         bt = q.t, bu = q.u, bv = q.v;
         return q.best;

@@ -64,7 +64,7 @@ __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame
     if (COUNT && query) cnt.c[any ? 1 : 0]++;
     float t = 0.f, u = 0.f, v = 0.f;
     const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
-    const int res = query ? traverse<FULL, COUNT>(sc, L.ray, any, stk, t, u, v, cnt) : -1;
+    const int res = query ? traverse<FULL, COUNT>(sc, L.ray, any, stk, t, u, v, cnt, cull_near_for(L)) : -1;
     const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t act = resolve<COUNT>(L, res, t, u, v, sc, fr, fb, cnt);
     advance<COUNT>(L, act, sc, fr, fb, ls, cnt);
@@ -200,15 +200,15 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         if (L.state != ST_IDLE && !tracing && !has_res) {  // a new query: begin its walk
             q_any = is_shadow_state(L.state);
             if (COUNT && L.state != ST_DEFER) cnt.c[q_any ? 1 : 0]++;
-            ri = ray_inv(L.ray);
+            ri = ray_inv(L.ray, cull_near_for(L));
             if (L.state == ST_DEFER) {  // no query: the deferred action runs in this shading step
                 res = -1;
                 has_res = true;
             } else if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root (bvh.h:277, :287)
                 res = -1, rt = L.ray.max_t, ru = rv = 0.f;
                 has_res = true;
-            } else if (FULL || !ri.fast) {
-                const TravResult q = traverse_binary<COUNT, Stack>(P->sc, L.ray, q_any, !FULL, stk);
+            } else if (FULL || !ri.fast || far_origin(P->sc, L.ray.o)) {  // the reference's tree, unculled
+                const TravResult q = traverse_binary<COUNT, Stack>(P->sc, L.ray, q_any, false, stk);
                 if (COUNT) cnt.c[2] += q.nodes, cnt.c[3] += q.tris, cnt.c[15] += q.exact;
                 res = q.best, rt = q.t, ru = q.u, rv = q.v;
                 has_res = true;

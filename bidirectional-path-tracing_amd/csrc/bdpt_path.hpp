@@ -751,6 +751,17 @@ __device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame
 
 __device__ __forceinline__ bool is_shadow_state(uint32_t st) { return st == ST_SPLAT || st == ST_NEE || st == ST_CONN; }
 
+// The near-cull threshold of the lane's pending query (kGrazeCos,
+// bdpt_device.hpp): none for a query that leaves the current vertex nearly
+// parallel to its surface, or the emitter (the first light-subpath ray, whose
+// sampled cosine is not kept); camera queries keep it.
+__device__ __forceinline__ float cull_near_for(const Lane& L) {
+    const uint32_t st = L.state;
+    if (st == ST_PRIMARY || st == ST_SPLAT) return kCullNear;
+    if (st == ST_LIGHT && L.c.depth == 1) return kNoCullNear;
+    return fabsf(dot(L.ray.d, L.h.n)) < kGrazeCos ? kNoCullNear : kCullNear;
+}
+
 // Applies the result of the lane's pending query (closest hit: leaf-order
 // triangle index res >= 0 with t, u, v; shadow ray: res >= 0 = occluded) and
 // returns the action the state machine continues with.

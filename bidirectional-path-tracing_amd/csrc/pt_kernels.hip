@@ -695,12 +695,12 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
         // PT_SHADE_READY of the wave have one, then advance together.
         if (L.busy && !tracing && !has_res) {
             if (COUNT) cnt.c[0]++;
-            ri = ray_inv(L.ray);
+            ri = ray_inv(L.ray, kCullNear);
             if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root (bvh.h:277, :287)
                 res = -1, rt = L.ray.max_t, ru = rv = 0.f;
                 has_res = true;
-            } else if (!ri.fast) {
-                const TravResult q = traverse_binary<COUNT, Stack>(P.sc, L.ray, false, true, stk);
+            } else if (!ri.fast || far_origin(P.sc, L.ray.o)) {  // the reference's tree, unculled
+                const TravResult q = traverse_binary<COUNT, Stack>(P.sc, L.ray, false, false, stk);
                 if (COUNT) cnt.c[2] += q.nodes, cnt.c[3] += q.tris, cnt.c[15] += q.exact;
                 res = q.best, rt = q.t, ru = q.u, rv = q.v;
                 has_res = true;
