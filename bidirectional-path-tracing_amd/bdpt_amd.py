@@ -211,6 +211,7 @@ def lib():
         L.bdpt_scene_get_info.argtypes = [vp, ctypes.POINTER(_SceneInfo)]
         L.bdpt_scene_export.argtypes = [vp, vp, vp, vp, vp]
         L.bdpt_scene_export_traversal.argtypes = [vp, vp, vp, vp, vp]
+        L.bdpt_intersect_from.argtypes = [vp, ctypes.c_int64, vp, vp, i32, vp]
         L.bdpt_scene_create.argtypes = [ctypes.POINTER(_SceneDesc), ctypes.POINTER(vp)]
         L.bdpt_scene_export_layout.argtypes = [vp, i32, vp, ctypes.POINTER(ctypes.c_int64)]
         L.bdpt_camera_constants.argtypes = [ctypes.POINTER(_Camera), i32, i32, f32p]
@@ -667,12 +668,19 @@ class BDPTIntegrator:
                                       wi.ctypes.data, pdf.ctypes.data))
         return f, wi, pdf
 
-    def intersect(self, rays, occlusion: bool = False) -> np.ndarray:
+    def intersect(self, rays, occlusion: bool = False, origin_normals=None) -> np.ndarray:
         """AcceleratorBVH::intersect (accel.h:125-172) or the occlusion query of
-        visibilityQuery (bvh.h:259-352) on rays (n, 8): a structured bdpt_hit array."""
+        visibilityQuery (bvh.h:259-352) on rays (n, 8): a structured bdpt_hit array.
+        origin_normals (n, 3): the surfaces the rays leave, for the frames' near-cull
+        rule (bdpt_intersect_from); None: no near cull."""
         r = _af32(rays, 8)
         out = np.zeros(r.shape[0], HIT_DTYPE)
-        _check(lib().bdpt_intersect(self._h, r.shape[0], r.ctypes.data, 1 if occlusion else 0, out.ctypes.data))
+        if origin_normals is None:
+            _check(lib().bdpt_intersect(self._h, r.shape[0], r.ctypes.data, 1 if occlusion else 0, out.ctypes.data))
+        else:
+            nr = _af32(origin_normals, 3)
+            _check(lib().bdpt_intersect_from(self._h, r.shape[0], r.ctypes.data, nr.ctypes.data, 1 if occlusion else 0,
+                                             out.ctypes.data))
         return out
 
     def splat_to_image_plane(self, points) -> np.ndarray:

@@ -35,8 +35,8 @@ hipError_t launch_bsdf_kat(const dev::DevScene& sc, int mode, int64_t n, const i
                            const float* x, float* out, hipStream_t st);
 hipError_t launch_fresnel_kat(int64_t n, const float* in, float* out, hipStream_t st);
 hipError_t launch_triangle_kat(int64_t n, const float* rays, const float* verts, float* out, hipStream_t st);
-hipError_t launch_intersect_kat(const dev::DevScene& sc, int64_t n, int occlusion, const float* rays, uint2* gstack,
-                                uint32_t nslots, float* out, hipStream_t st);
+hipError_t launch_intersect_kat(const dev::DevScene& sc, int64_t n, int occlusion, const float* rays, const float* nrm,
+                                uint2* gstack, uint32_t nslots, float* out, hipStream_t st);
 hipError_t launch_splat_kat(const dev::DevFrame& fr, int64_t n, const float* p, int32_t* xy, hipStream_t st);
 int frame_kernel_lds_stack();
 int frame_kernel_blocks_per_cu(size_t dyn_lds);
@@ -1109,6 +1109,11 @@ int bdpt_bsdf_type(const bdpt_scene* s, int32_t mat, uint32_t* type, int32_t* ki
 }
 
 int bdpt_intersect(bdpt_ctx* c, int64_t n, const float* rays, int32_t occlusion, bdpt_hit* out) {
+    return bdpt_intersect_from(c, n, rays, nullptr, occlusion, out);
+}
+
+int bdpt_intersect_from(bdpt_ctx* c, int64_t n, const float* rays, const float* origin_normals, int32_t occlusion,
+                        bdpt_hit* out) {
     static_assert(sizeof(bdpt_hit) == 20 * 4, "bdpt_hit is the kernel's 20-word record");
     if (!c || n < 0 || (n > 0 && (!rays || !out))) return fail(BDPT_ERR_INVALID, "bad argument");
     if (n == 0) return BDPT_OK;
@@ -1116,9 +1121,10 @@ int bdpt_intersect(bdpt_ctx* c, int64_t n, const float* rays, int32_t occlusion,
     int rc;
     if ((rc = begin_use(c, c->stream))) return rc;
     KatBuffers kb;
-    void *dr, *dout;
+    void *dr, *dout, *dn = nullptr;
     const size_t N = static_cast<size_t>(n);
     if ((rc = kat_in(c, kb, rays, 32 * N, &dr)) || (rc = kat_in(c, kb, nullptr, 80 * N, &dout))) return rc;
+    if (origin_normals && (rc = kat_in(c, kb, origin_normals, 12 * N, &dn))) return rc;
     // The interior-box test the frame kernels would use for these origins: without
     // the ambiguity slack when every origin lies within 100 scene diagonals (as
     // for a frame whose camera does, node_slack_needed), with it otherwise.
@@ -1129,8 +1135,9 @@ int bdpt_intersect(bdpt_ctx* c, int64_t n, const float* rays, int32_t occlusion,
     // the traversal-stack overflow columns serve c->nslots rays at a time
     for (int64_t b = 0; b < n; b += c->nslots) {
         const int64_t m = std::min<int64_t>(c->nslots, n - b);
-        HIP_TRY(launch_intersect_kat(sc, m, occlusion ? 1 : 0, static_cast<const float*>(dr) + 8 * b, c->gstack,
-                                     c->nslots, static_cast<float*>(dout) + 20 * b, c->stream));
+        HIP_TRY(launch_intersect_kat(sc, m, occlusion ? 1 : 0, static_cast<const float*>(dr) + 8 * b,
+                                     dn ? static_cast<const float*>(dn) + 3 * b : nullptr, c->gstack, c->nslots,
+                                     static_cast<float*>(dout) + 20 * b, c->stream));
     }
     HIP_TRY(hipMemcpyAsync(out, dout, 80 * N, hipMemcpyDeviceToHost, c->stream));
     if ((rc = end_use(c, c->stream))) return rc;

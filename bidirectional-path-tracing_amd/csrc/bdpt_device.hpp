@@ -507,9 +507,11 @@ constexpr float kCullNear = BDPT_CULL_NEAR ? 5e-4f : -__builtin_huge_valf();
 // triangle. For a ray nearly parallel to a triangle's plane whose origin lies on
 // that plane (a grazing ray leaving a surface) the computed t, u, v are rounding
 // noise the reference still accepts (t > 1e-3), so such queries walk without the
-// near cull: every query leaving a surface at |cos| < kGrazeCos to its shading
-// normal, and the first light-subpath ray.
-constexpr float kGrazeCos = 0.1f;
+// near cull: every query leaving a surface (a path vertex or the emitter) at
+// |cos| < kGrazeCos to its shading normal. Below it the
+// t error of a coplanar triangle, ~1.2e-7 |o - v0| / (|cos| sin(corner)), can
+// pass 1e-3 only for triangles with a corner under ~0.35 degrees.
+constexpr float kGrazeCos = 0.02f;
 enum : int { kSlabMiss = 0, kSlabHit = 1, kSlabAmbiguous = 2 };
 struct RayInv {
     f3 inv;

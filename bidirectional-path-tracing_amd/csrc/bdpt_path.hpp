@@ -470,6 +470,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         f3 fs, ft;
         make_frame(e_n, fs, ft);
         L.ray = Ray{e_p, to_world(fs, ft, e_n, edir), kEpsilon, 3.402823466e+38f};
+        L.h.n = e_n;  // the surface the first light ray leaves (cull_near_for); the walk's resolve overwrites L.h
         L.c.tp = (ld3(e.radiance) * edir.z) * rcp_cr(emissionPdf);
         L.c.vc = edir.z * rcp_cr(emissionPdf);
         L.c.vcm = div_cr(areaPdf, emissionPdf);
@@ -752,13 +753,12 @@ __device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame
 __device__ __forceinline__ bool is_shadow_state(uint32_t st) { return st == ST_SPLAT || st == ST_NEE || st == ST_CONN; }
 
 // The near-cull threshold of the lane's pending query (kGrazeCos,
-// bdpt_device.hpp): none for a query that leaves the current vertex nearly
-// parallel to its surface, or the emitter (the first light-subpath ray, whose
-// sampled cosine is not kept); camera queries keep it.
+// bdpt_device.hpp): none for a query that leaves the current vertex (or, for the
+// first light-subpath ray, the emitter: A_START_LIGHT puts its normal in L.h.n)
+// nearly parallel to its surface; camera queries keep it.
 __device__ __forceinline__ float cull_near_for(const Lane& L) {
     const uint32_t st = L.state;
     if (st == ST_PRIMARY || st == ST_SPLAT) return kCullNear;
-    if (st == ST_LIGHT && L.c.depth == 1) return kNoCullNear;
     return fabsf(dot(L.ray.d, L.h.n)) < kGrazeCos ? kNoCullNear : kCullNear;
 }
 

@@ -72,8 +72,12 @@ __global__ __launch_bounds__(kKatBlock) void triangle_kat_kernel(int64_t n, cons
 // &info, true), as visibilityQuery calls it) through the product traversal.
 // out per ray (20 words, bdpt_hit): hit (int bits), t, u, v, shapeID, primID, matID (int bits),
 // p[3], frameNs.n[3], frameNg.n[3], wo[3], leaf-order triangle index (int bits).
+// nrm (optional, 3 per ray): the normal of the surface the ray leaves, for the
+// frame kernels' near-cull rule (cull_near_for: a zero normal = a camera
+// origin); without it no box is near-culled.
 __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, int64_t n, int occlusion,
                                                                  const float* __restrict__ rays,
+                                                                 const float* __restrict__ nrm,
                                                                  uint2* __restrict__ gstack, uint32_t nslots,
                                                                  float* __restrict__ out) {
     __shared__ uint2 stack_mem[kLdsStack * kKatBlock];
@@ -86,7 +90,13 @@ __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, i
     const Ray ray{mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], r[7]};
     Counts cnt;
     float t = 0.f, u = 0.f, v = 0.f;
-    const int res = traverse<false, false>(sc, ray, occlusion != 0, stk, t, u, v, cnt);
+    float near = kNoCullNear;
+    if (nrm) {
+        const f3 sn = mk(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]);
+        const bool camera = sn.x == 0.f && sn.y == 0.f && sn.z == 0.f;
+        near = (camera || !(fabsf(dot(ray.d, sn)) < kGrazeCos)) ? kCullNear : kNoCullNear;
+    }
+    const int res = traverse<false, false>(sc, ray, occlusion != 0, stk, t, u, v, cnt, near);
     float* o = out + 20 * i;
     for (int k = 0; k < 20; k++) o[k] = 0.f;
     if (occlusion) {
@@ -139,11 +149,12 @@ hipError_t launch_triangle_kat(int64_t n, const float* rays, const float* verts,
         hipLaunchKernelGGL(dev::triangle_kat_kernel, kat_grid(n), dim3(dev::kKatBlock), 0, st, n, rays, verts, out);
     return hipGetLastError();
 }
-hipError_t launch_intersect_kat(const dev::DevScene& sc, int64_t n, int occlusion, const float* rays, uint2* gstack,
-                                uint32_t nslots, float* out, hipStream_t st) {
+hipError_t launch_intersect_kat(const dev::DevScene& sc, int64_t n, int occlusion, const float* rays, const float* nrm,
+                                uint2* gstack, uint32_t nslots, float* out, hipStream_t st) {
     if (n > 0)
         hipLaunchKernelGGL(dev::intersect_kat_kernel, kat_grid(n), dim3(dev::kKatBlock),
-                           4 * static_cast<size_t>(sc.lds_words), st, sc, n, occlusion, rays, gstack, nslots, out);
+                           4 * static_cast<size_t>(sc.lds_words), st, sc, n, occlusion, rays, nrm, gstack, nslots,
+                           out);
     return hipGetLastError();
 }
 hipError_t launch_splat_kat(const dev::DevFrame& fr, int64_t n, const float* p, int32_t* xy, hipStream_t st) {

@@ -383,10 +383,18 @@ typedef struct {
 /* rays: n x 8 (o.xyz d.xyz min_t max_t). occlusion = 0: closest hit (accel.h:125);
  * 1: the any-hit query of visibilityQuery (bvh.h:259-352 with occlusion = true),
  * result in hit only. The traversal is the frame kernels' (culled 4-wide tree,
- * reference-leaf check), with the interior-box test a frame would use for the
- * batch's origins: without the ambiguity slack when all lie within 100 scene
- * diagonals, with it otherwise. */
+ * reference-leaf check; origins beyond 100 scene diagonals walk the reference's
+ * tree unculled), with the interior-box test a frame would use for the batch's
+ * origins: without the ambiguity slack when all lie within 100 scene diagonals,
+ * with it otherwise. */
 int bdpt_intersect(bdpt_ctx* ctx, int64_t n, const float* rays, int32_t occlusion, bdpt_hit* out);
+/* The same with the frame kernels' near-cull rule: origin_normals (n x 3) is the
+ * normal of the surface each ray leaves (a path vertex's shading normal, the
+ * emitter's normal), zero for a camera origin. bdpt_intersect (origin_normals
+ * NULL) culls no box for lying close to the origin; the frames skip such boxes
+ * unless the query leaves its surface at |cos| < 0.02. */
+int bdpt_intersect_from(bdpt_ctx* ctx, int64_t n, const float* rays, const float* origin_normals, int32_t occlusion,
+                        bdpt_hit* out);
 /* BDPTIntegrator::splatToImagePlane (bdpt.h:485-496) of points p (n x 3) for the
  * camera and image of params: xy = n x 2 (the reference's int truncation). */
 int bdpt_splat_to_image_plane(bdpt_ctx* ctx, const bdpt_frame_params* params, int64_t n, const float* p,

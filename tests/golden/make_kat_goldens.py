@@ -203,7 +203,8 @@ def adversarial_rays(scene, n, seed):
     """Rays chosen where the product traversal's exactness argument is thinnest
     (DESIGN.md §2 items 5-6): the computed hit of Moller-Trumbore near |det| = 1e-8,
     ties between triangles sharing an edge or a vertex, origins on surfaces, and
-    origins beyond 100 scene diagonals. Returns (rays [n, 8] float32, kind [n])."""
+    origins beyond 100 scene diagonals. Returns (rays [n, 8] float32, kind [n],
+    the normal of the triangle a ray leaves [n, 3] (0 for camera / free / far origins))."""
     sys.path.insert(0, os.path.join(REPO, "bidirectional-path-tracing_amd"))
     import bdpt_amd
 
@@ -224,10 +225,11 @@ def adversarial_rays(scene, n, seed):
     curved = np.flatnonzero(ti[:, 0] == shapes[np.argmax(counts)])  # the tessellated sphere(s)
     FLT_MAX = 3.402823466e38
     k = n // 6
-    out, kind = [], []
+    out, kind, onrm = [], [], []
 
-    def add(o, d, mn, mx, tag):
+    def add(o, d, mn, mx, tag, nrm=None):
         m = o.shape[0]
+        onrm.append(np.zeros((m, 3), f32) if nrm is None else np.asarray(nrm, f32))
         out.append(np.concatenate([o, _normalize(d), np.broadcast_to(np.float32(mn), (m, 1)) if np.isscalar(mn)
                                    else mn[:, None], np.broadcast_to(np.float32(mx), (m, 1)) if np.isscalar(mx)
                                    else mx[:, None]], 1).astype(f32))
@@ -239,10 +241,11 @@ def adversarial_rays(scene, n, seed):
     t1 = _normalize(e1[idx])
     t2 = _normalize(np.cross(ng[idx], t1))
     phi = rng.random(k) * 2 * np.pi
-    delta = rng.choice([0.0, 1e-9, 3e-9, 1e-8, 3e-8, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2], k) * rng.choice([-1, 1], k)
+    delta = rng.choice([0.0, 1e-9, 3e-9, 1e-8, 3e-8, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2, 0.015, 0.02, 0.03, 0.05],
+                       k) * rng.choice([-1, 1], k)
     d = t1 * np.cos(phi)[:, None] + t2 * np.sin(phi)[:, None] + ng[idx] * delta[:, None]
     h = rng.choice([0.0, 0.0, 1e-7, -1e-7, 1e-6, -1e-6, 1e-5, 1e-4], k)
-    add((o + ng[idx] * h[:, None]).astype(f32), d, 1e-8, FLT_MAX, 0)
+    add((o + ng[idx] * h[:, None]).astype(f32), d, 1e-8, FLT_MAX, 0, ng[idx])
     # 1: grazing shadow segments between two points of the same large triangle (visibilityQuery)
     idx = rng.choice(big, k)
     a, b = _surface_points(rng, tri, idx), _surface_points(rng, tri, idx)
@@ -251,7 +254,7 @@ def adversarial_rays(scene, n, seed):
     dd = (b - a).astype(f32)
     dist = np.sqrt((dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1]) + dd[:, 2] * dd[:, 2]).astype(f32)
     keep = dist > 1e-4
-    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 1)
+    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 1, ng[idx][keep])
     # 2: rays through the curved mesh's vertices and edges (ties between neighbours, silhouettes)
     idx = rng.choice(curved, k)
     w = rng.choice(4, k)
@@ -269,7 +272,7 @@ def adversarial_rays(scene, n, seed):
     flat = rng.random(k) < 0.3
     d[flat] -= ng[idx][flat] * np.sum(d[flat] * ng[idx][flat], 1, keepdims=True) * (1 - rng.choice(
         [1e-6, 1e-4, 1e-2], flat.sum()))[:, None]
-    add(o, d, 1e-8, FLT_MAX, 3)
+    add(o, d, 1e-8, FLT_MAX, 3, ng[idx])
     # 4: origins 100 - 10000 scene diagonals away, aimed at surface points (the slack-test regime)
     dirn = rng.normal(size=(k, 3))
     dirn /= np.linalg.norm(dirn, axis=1, keepdims=True)
@@ -280,19 +283,20 @@ def adversarial_rays(scene, n, seed):
     add(o, tgt - o, np.where(rng.random(k) < 0.5, 1.0, 1e-8).astype(f32), mx, 4)
     # 5: shadow segments between surface points of any two triangles
     m = n - 5 * k
-    a = _surface_points(rng, tri, rng.integers(0, tri.shape[0], m))
+    ia = rng.integers(0, tri.shape[0], m)
+    a = _surface_points(rng, tri, ia)
     b = _surface_points(rng, tri, rng.integers(0, tri.shape[0], m))
     dd = (b - a).astype(f32)
     dist = np.sqrt((dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1]) + dd[:, 2] * dd[:, 2]).astype(f32)
     keep = dist > 1e-4
-    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 5)
-    return np.concatenate(out), np.concatenate(kind)
+    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 5, ng[ia][keep])
+    return np.concatenate(out), np.concatenate(kind), np.concatenate(onrm)
 
 
 def adversarial_fixture(scene, n, seed):
-    rays, kind = adversarial_rays(scene, n, seed)
+    rays, kind, onrm = adversarial_rays(scene, n, seed)
     out = kat(toml(scene), 64, 64, "intersect", rays, 21)
-    np.savez_compressed(os.path.join(HERE, f"kat_adversarial_{scene}.npz"), rays=rays, kind=kind,
+    np.savez_compressed(os.path.join(HERE, f"kat_adversarial_{scene}.npz"), rays=rays, kind=kind, onrm=onrm,
                         hit=out[:, 0].astype(np.int8), t=out[:, 1], u=out[:, 2], v=out[:, 3],
                         shape=out[:, 4].view(np.int32), prim=out[:, 5].view(np.int32),
                         occluded=out[:, 20].astype(np.int8))

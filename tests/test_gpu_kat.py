@@ -119,13 +119,18 @@ def test_gpu_intersect_adversarial_rays_match_reference(scene):
     starting on surfaces, and origins 100 - 10000 scene diagonals away. Closest
     hit (acceptance, t, u, v, shape, prim) and occlusion bit for bit against the
     reference's AcceleratorBVH; the in-scene batches run the frames' slack-free
-    interior test, the far batch and the mixed batch the slack test."""
+    interior test, the far batch and the mixed batch the slack test (far origins
+    themselves walk the reference's tree), each without the near cull and with
+    the frames' near-cull rule."""
     g = kat(f"kat_adversarial_{scene}")
     it = integrator(scene)
-    rays, kind = g["rays"], g["kind"]
+    rays, kind, onrm = g["rays"], g["kind"], g["onrm"]
     far = kind == 4
-    for sel in (~far, far, np.ones_like(far)):
-        h = it.intersect(rays[sel])
+    # without the near cull (bdpt_intersect), then with the frames' rule given the
+    # surfaces the rays leave (bdpt_intersect_from: near cull unless |cos| < 0.02)
+    for sel, nrm in ((~far, None), (far, None), (np.ones_like(far), None), (~far, onrm[~far]),
+                     (np.ones_like(far), onrm)):
+        h = it.intersect(rays[sel], origin_normals=nrm)
         hit = g["hit"][sel].astype(np.int32)
         bad = np.flatnonzero(h["hit"] != hit)
         assert bad.size == 0, f"{bad.size} acceptance mismatches, kinds {np.bincount(kind[sel][bad])}"
@@ -134,7 +139,7 @@ def test_gpu_intersect_adversarial_rays_match_reference(scene):
         assert same_bits(h["v"][k], g["v"][sel][k])
         assert np.array_equal(h["shape_id"][k], g["shape"][sel][k]) and np.array_equal(h["prim_id"][k],
                                                                                           g["prim"][sel][k])
-        occ = it.intersect(rays[sel], occlusion=True)
+        occ = it.intersect(rays[sel], occlusion=True, origin_normals=nrm)
         bad = np.flatnonzero(occ["hit"] != g["occluded"][sel].astype(np.int32))
         assert bad.size == 0, f"{bad.size} occlusion mismatches, kinds {np.bincount(kind[sel][bad])}"
 

@@ -23,14 +23,18 @@ for scene in ("caustic", "hardlight", "synth1m"):
     it.init()
     rays, kind = g["rays"], g["kind"]
     res = {}
-    for name, sel in (("near", kind != 4), ("far", kind == 4), ("all", np.ones_like(kind, bool))):
-        h = it.intersect(rays[sel])
-        o = it.intersect(rays[sel], occlusion=True)
+    for name, sel, rule in (("near", kind != 4, False), ("far", kind == 4, False), ("all", kind >= 0, False),
+                            ("near_rule", kind != 4, True), ("all_rule", kind >= 0, True)):
+        nrm = g["onrm"][sel] if rule else None
+        h = it.intersect(rays[sel], origin_normals=nrm)
+        o = it.intersect(rays[sel], occlusion=True, origin_normals=nrm)
         res[name + "_t"], res[name + "_u"], res[name + "_v"] = h["t"], h["u"], h["v"]
         res[name + "_hit"], res[name + "_tri"], res[name + "_occ"] = h["hit"], h["tri"], o["hit"]
         res[name + "_shape"], res[name + "_prim"] = h["shape_id"], h["prim_id"]
         k = g["hit"][sel] == 1
         bad = (h["t"][k].view(np.uint32) != g["t"][sel][k].view(np.uint32))
+        obad = o["hit"] != g["occluded"][sel]
         print(scene, name, "hits", int(k.sum()), "t mismatches", int(bad.sum()), "per kind",
-              np.bincount(kind[sel][k][bad], minlength=6).tolist(), flush=True)
+              np.bincount(kind[sel][k][bad], minlength=6).tolist(), "occlusion mismatches", int(obad.sum()),
+              np.bincount(kind[sel][obad], minlength=6).tolist(), flush=True)
     np.savez_compressed(os.path.join(out, f"adv_{scene}.npz"), **res)
