@@ -439,16 +439,6 @@ __device__ __forceinline__ void make_frame(f3 a, f3& s, f3& t) {
 #endif
     s = cross(t, a);
 }
-// The t axis of Frame(a) alone (the part that costs a square root and a
-// reciprocal); s = cross(t, a) is recomputed from it bit for bit (local_with).
-__device__ __forceinline__ f3 frame_t(f3 a) {
-    if (fabsf(a.x) > fabsf(a.y)) {
-        const float inv = rcp_cr(sqrt_cr(a.x * a.x + a.z * a.z));
-        return mk(a.z * inv, 0.f, -a.x * inv);
-    }
-    const float inv = rcp_cr(sqrt_cr(a.y * a.y + a.z * a.z));
-    return mk(0.f, a.z * inv, -a.y * inv);
-}
 __device__ __forceinline__ f3 to_local(f3 s, f3 t, f3 n, f3 v) { return mk(dot(v, s), dot(v, t), dot(v, n)); }
 __device__ __forceinline__ f3 to_world(f3 s, f3 t, f3 n, f3 v) { return (s * v.x + t * v.y) + n * v.z; }
 __device__ __forceinline__ f3 reflect_z(f3 d) { return mk(-d.x, -d.y, d.z); }
@@ -459,9 +449,6 @@ __device__ __forceinline__ f3 local_at(f3 n, f3 v) {
     make_frame(n, s, t);
     return to_local(s, t, n, v);
 }
-// The same with the frame's t axis already known (frame_t(n)).
-__device__ __forceinline__ f3 local_with(f3 t, f3 n, f3 v) { return to_local(cross(t, n), t, n, v); }
-__device__ __forceinline__ f3 world_with(f3 t, f3 n, f3 v) { return to_world(cross(t, n), t, n, v); }
 __device__ __forceinline__ f3 world_at(f3 n, f3 v) {
     f3 s, t;
     make_frame(n, s, t);

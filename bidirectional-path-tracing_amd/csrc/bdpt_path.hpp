@@ -15,13 +15,7 @@ namespace bdpt {
 namespace dev {
 
 
-#ifndef BDPT_LV_FRAME
-#define BDPT_LV_FRAME 0  // 1: light-vertex records carry their shading frame's t axis (a 5th float4)
-#endif
-#ifndef BDPT_EYE_FRAME
-#define BDPT_EYE_FRAME 0  // 1: the eye vertex's frame t axis is kept in the cold lane state (cam_d's slot)
-#endif
-constexpr int kLvFields = BDPT_LV_FRAME ? 20 : 16;  // p vcm n vc wo rr tp mat [t]
+constexpr int kLvFields = 16;  // p vcm n vc wo rr tp mat
 constexpr uint32_t kFlagNoEyeAccum = 0x100u;  // single-sample API: Li is returned, not added
 // Safety bound on the queries of one sample: a legal sample issues at most D
 // light-walk rays, D camera splats, D eye-walk rays and, per eye vertex, one
@@ -66,7 +60,7 @@ struct LightStore {
     float4* __restrict__ base;
     uint32_t maxv, slot;
     __device__ __forceinline__ float4* at(int v) const {
-        return base + (static_cast<size_t>(slot) * maxv + static_cast<uint32_t>(v)) * (kLvFields / 4);
+        return base + (static_cast<size_t>(slot) * maxv + static_cast<uint32_t>(v)) * 4;
     }
 };
 __device__ __forceinline__ LightStore light_store(float* lv, int lv_max, uint32_t slot) {
@@ -78,8 +72,6 @@ struct Vertex {  // PathVertex (bdpt.h:24-35); its Frame is rebuilt from n where
     float vcm, vc, rr;
     int mat;
 };
-// The shading frame's t axis of light vertex v (BDPT_LV_FRAME records).
-__device__ __forceinline__ f3 load_vertex_t(const LightStore& ls, int v) { return xyz(gld4(ls.at(v) + 4)); }
 
 #ifndef BDPT_LV_NT
 #define BDPT_LV_NT 0  // 1: light-vertex records use non-temporal loads / stores (keep L2 for the scene)
@@ -126,8 +118,7 @@ __device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
 // ContinuePathRandomWalk (bdpt.h:243-291): BSDF sample (2 draws), throughput,
 // vc / vcm recursion (Georgiev VCM Eqs. 52-54) and the next ray.
 __device__ __forceinline__ bool continue_walk(const BsdfRecord& b, const Hit& h, LazyMT& rng, f3& tp, int& depth,
-                                              float& vc, float& vcm, Ray& ray, float rrp, bool have_t = false,
-                                              f3 t = f3{0.f, 0.f, 0.f}) {
+                                              float& vc, float& vcm, Ray& ray, float rrp) {
     const bool delta = is_delta(b);
     float pdf;
     f3 wi;
@@ -145,7 +136,7 @@ __device__ __forceinline__ bool continue_walk(const BsdfRecord& b, const Hit& h,
         vc = div_cr(absCosOut, pdf) * (vcm + prevRev * vc);
         vcm = rcp_cr(pdf);
     }
-    ray = Ray{h.p, have_t ? world_with(t, h.n, wi) : world_at(h.n, wi), kEpsilon, 3.402823466e+38f};  // FLT_MAX (core.h:120)
+    ray = Ray{h.p, world_at(h.n, wi), kEpsilon, 3.402823466e+38f};  // FLT_MAX (core.h:120)
     return true;
 }
 
@@ -218,7 +209,6 @@ enum : uint32_t {  // actions that need no query
     A_START_EYE,
     A_EYE_NEXT,
     A_EYE_VERTEX,
-    A_CONN_SHADE,  // BDPT_CONN_AFTER_VIS: connectVertices' contribution after an unoccluded shadow ray
     A_CONN,
     A_EYE_CONTINUE,
     A_FINISH,
@@ -333,37 +323,6 @@ __device__ __forceinline__ void tally_action(Counts& cnt, bool on) {
     }
 }
 
-#ifndef BDPT_CONN_AFTER_VIS
-#define BDPT_CONN_AFTER_VIS 0  // 1: connectVertices evaluates BSDFs and MIS only after an unoccluded shadow ray
-#endif
-
-// connectVertices' contribution (bdpt.h:455-482) for light vertex V seen from
-// the eye vertex in L along dir (light -> eye), cosines already accepted.
-__device__ __forceinline__ f3 conn_contrib(const Lane& L, const Vertex& V, const BsdfRecord& be, const BsdfRecord& bl,
-                                           f3 dir, float invD2, float cosL, float cosE, const LightStore& ls,
-                                           const DevFrame& fr) {
-#if BDPT_LV_FRAME
-    const f3 wiL = local_with(load_vertex_t(ls, L.c.ci), V.n, dir);
-#else
-    const f3 wiL = local_at(V.n, dir);  // Frame(n) is a pure function of n
-#endif
-    const f3 wiE = BDPT_EYE_FRAME ? local_with(L.c.cam_d, L.h.n, -dir) : local_at(L.h.n, -dir);
-    const EvalPdfs eL = bsdf_eval_pdfs(bl, wiL, V.wo), eE = bsdf_eval_pdfs(be, wiE, L.h.wo);
-    f3 Li = eL.f * eE.f;
-    Li = Li * ((V.tp * L.c.tp) * invD2);
-    const float rrL = rr_on(fr) ? V.rr : 1.f, rrE = rr_on(fr) ? L.c.rr : 1.f;  // bdpt.h:461-472
-    const float eyePathRev_w = eL.fwd * rrL;
-    const float lightPrevRev = eL.rev * rrL;
-    const float lightPathRev_w = eE.fwd * rrE;
-    const float eyePrevRev = eE.rev * rrE;
-    const float lightPathRev_a = lightPathRev_w * cosL * invD2;
-    const float eyePathRev_a = eyePathRev_w * cosE * invD2;
-    const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
-    const float eyeWeight = eyePathRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
-    const float mis = rcp_cr(lightWeight + 1.f + eyeWeight);
-    return Li * mis;
-}
-
 // The subpath loop test of bdpt.h:68 / :188. With Russian roulette a subpath
 // that reaches DevFrame::depth_cap (the light-vertex store's bound) ends there
 // and the sample is counted in *capped (the frame is then not the reference's).
@@ -449,7 +408,6 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         }
         L.c.pure = 0u;
         L.c.ci = 0;
-        if (BDPT_EYE_FRAME) L.c.cam_d = frame_t(L.h.n);  // cam_d is dead once the eye walk started
         act = A_NEE;
     } BDPT_END;
     // The emitter sample (4 draws) of lightSubpathWalk (bdpt.h:162-163) and of
@@ -495,7 +453,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const float cosAtLight = dot(e_n, dir);
         const float cosAtEye = dot(-dir, L.h.n);  // = the frame's z component (to_local)
         if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
-        const f3 wi = BDPT_EYE_FRAME ? local_with(L.c.cam_d, L.h.n, -dir) : local_at(L.h.n, -dir);
+        const f3 wi = local_at(L.h.n, -dir);
 #else
         const f3 wi = local_at(L.h.n, -dir);
         const float cosAtLight = dot(e_n, dir);
@@ -526,12 +484,6 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         if (rr_on(fr)) L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);  // bdpt.h:201-204
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         if (is_delta(b)) break;
-#if BDPT_LV_FRAME
-        // the frame's t axis goes with the vertex record (slot nl: the vertex is
-        // stored there if its BSDF sample succeeds), read back by its connections
-        const f3 tl = frame_t(L.h.n);
-        lv_st(ls.at(L.c.nl) + 4, make_float4(tl.x, tl.y, tl.z, 0.f));
-#endif
         // connectToCamera (bdpt.h:295-371): everything but the visibility test.
         f3 e2l = L.h.p - cam_o;
         const float invD2 = rcp_cr(dot(e2l, e2l));
@@ -543,11 +495,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         if (cosCamera <= 0.f) break;
 #if BDPT_CONN_EARLY_COS >= 3
         if (dot(-e2l, L.h.n) <= 0.f) break;  // wi.z <= 0 (the frame z component, to_local)
-#if BDPT_LV_FRAME
-        const f3 wi = local_with(tl, L.h.n, -e2l);
-#else
         const f3 wi = local_at(L.h.n, -e2l);
-#endif
         const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
         const f3 f = ep.f;
         if (is_zero(f)) break;
@@ -576,39 +524,6 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         L.state = ST_SPLAT;
         act = A_ISSUED;
     } BDPT_END;
-#if BDPT_CONN_AFTER_VIS
-    // The reference's own order (bdpt.h:447-456): cosines, the shadow ray, then
-    // (unoccluded only) the BSDF evaluations and weights, added to Li in ci order.
-    BDPT_ACTION(27, act == A_CONN_SHADE) {
-        const Vertex V = load_vertex(ls, L.c.ci);
-        f3 dir = L.h.p - V.p;
-        const float invD2 = rcp_cr(dot(dir, dir));
-        dir = dir * sqrt_cr(invD2);
-        const float cosL = dot(dir, V.n), cosE = dot(-dir, L.h.n);
-        L.c.Li = L.c.Li + conn_contrib(L, V, bsdf_of(sc, L.h.mat), bsdf_of(sc, V.mat), dir, invD2, cosL, cosE, ls, fr);
-        L.c.ci++;
-        act = A_CONN;
-    } BDPT_END;
-    BDPT_ACTION(27, act == A_CONN) {  // connectVertices (bdpt.h:434-451) with light vertex ci: up to the shadow ray
-        act = A_EYE_CONTINUE;
-        if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
-        while (L.c.ci < L.c.nl) {
-            const f3 vp = xyz(lv_ld(ls.at(L.c.ci))), vn = xyz(lv_ld(ls.at(L.c.ci) + 1));
-            if (COUNT) cnt.c[5]++;
-            f3 dir = L.h.p - vp;
-            const float invD2 = rcp_cr(dot(dir, dir));
-            dir = dir * sqrt_cr(invD2);
-            if (dot(dir, vn) <= 0.f || dot(-dir, L.h.n) <= 0.f) {  // the frames' z components (to_local)
-                L.c.ci++;
-                continue;
-            }
-            L.ray = shadow_ray(L.h.p, vp);
-            L.state = ST_CONN;
-            act = A_ISSUED;
-            break;
-        }
-    } BDPT_END;
-#else
     BDPT_ACTION(27, act == A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
         act = A_EYE_CONTINUE;
         if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
@@ -627,12 +542,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 L.c.ci++;
                 continue;
             }
-#if BDPT_LV_FRAME
-            const f3 wiL = local_with(load_vertex_t(ls, L.c.ci), V.n, dir);
-#else
             const f3 wiL = local_at(V.n, dir);  // Frame(n) is a pure function of n
-#endif
-            const f3 wiE = BDPT_EYE_FRAME ? local_with(L.c.cam_d, L.h.n, -dir) : local_at(L.h.n, -dir);
+            const f3 wiE = local_at(L.h.n, -dir);
 #else
             const f3 wiL = local_at(V.n, dir);  // Frame(n) is a pure function of n
             const f3 wiE = local_at(L.h.n, -dir);
@@ -663,7 +574,6 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             break;
         }
     } BDPT_END;
-#endif
     // ContinuePathRandomWalk of either subpath (light: bdpt.h:211-215, eye: bdpt.h:152).
     BDPT_ACTION(28, act == A_LIGHT_CONTINUE || act == A_EYE_CONTINUE) {
         const bool light = act == A_LIGHT_CONTINUE;
@@ -677,17 +587,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             break;
         }
         if (light && !delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, rrp);  // the pre-walk state
-#if BDPT_LV_FRAME || BDPT_EYE_FRAME
-        // the vertex's frame axis when a connection body already computed it
-        const bool have_t = !delta && (light ? BDPT_LV_FRAME : BDPT_EYE_FRAME);
-        f3 tc = L.c.cam_d;
-#if BDPT_LV_FRAME
-        if (light) tc = load_vertex_t(ls, L.c.nl);
-#endif
-        const bool more = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, rrp, have_t, tc);
-#else
         const bool more = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, rrp);
-#endif
         if (!light) {
             act = more ? A_EYE_NEXT : A_FINISH;
         } else if (more) {
@@ -798,18 +698,9 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
             act = A_CONN;
             break;
         case ST_CONN:
-#if BDPT_CONN_AFTER_VIS
-            if (!hit) {
-                act = A_CONN_SHADE;
-            } else {
-                L.c.ci++;
-                act = A_CONN;
-            }
-#else
             if (!hit) L.c.Li = L.c.Li + L.c.pend;
             L.c.ci++;
             act = A_CONN;
-#endif
             break;
         case ST_DEFER: act = A_START_EYE; break;
         default: act = A_DONE;
