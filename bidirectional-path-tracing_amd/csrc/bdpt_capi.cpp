@@ -318,6 +318,28 @@ int bdpt_device_count(int32_t* count) {
     return BDPT_OK;
 }
 
+// The BSDF records as the kernels read them. A MixtureBSDF with Ks == 0, scale
+// == 1 and a finite exponent >= 0 (so specw == 0) returns DiffuseBSDF's values
+// bit for bit (mixture.h:59-151 against diffuse.h:35-61): eval adds
+// (0 * (n + 2)) * INV_TWOPI * powf(c, n) = +0 (c in [0, 1], so powf is
+// finite) to Kd * INV_PI and multiplies by 1; pdf is pdfPhong * 0 + pdfDiffuse
+// * 1 with a finite pdfPhong; sample takes the diffuse branch (u.x < 0 never
+// holds) with (u.x - 0) / (1 - 0) == u.x. The kernels run it as diffuse, so a
+// wave whose lanes shade both kinds runs one branch instead of two.
+// BDPT_KEEP_MIXTURE=1 keeps the record as loaded (the A/B of DESIGN.md).
+static std::vector<BsdfRecord> device_bsdfs(const std::vector<BsdfRecord>& in) {
+    std::vector<BsdfRecord> out = in;
+    const char* keep = std::getenv("BDPT_KEEP_MIXTURE");
+    if (keep && *keep == '1') return out;
+    for (BsdfRecord& b : out) {
+        const bool ks0 = b.ks[0] == 0.f && b.ks[1] == 0.f && b.ks[2] == 0.f;
+        if (b.kind == BSDF_MIXTURE && ks0 && b.scale == 1.f && b.specw == 0.f && std::isfinite(b.exponent) &&
+            b.exponent >= 0.f)
+            b.kind = BSDF_DIFFUSE;  // type keeps the reference's flags (only its delta bits are read)
+    }
+    return out;
+}
+
 static int upload(bdpt_ctx* c, const void* src, size_t bytes, void** dst) {
     if (bytes == 0) bytes = 16;
     HIP_TRY(hipMalloc(dst, bytes));
@@ -374,11 +396,21 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     if ((rc = upload(c.get(), L.wnodes.data(), L.wnodes.size() * 16, &p))) return rc;
     c->sc.wnodes = static_cast<const float4*>(p);
     c->sc.wroot_link = L.wroot_link;
+    c->sc.qnodes = nullptr;
+    c->sc.q_ok = 0u;
+    if (L.q_ok) {
+        if ((rc = upload(c.get(), L.qnodes.data(), L.qnodes.size() * 16, &p))) return rc;
+        c->sc.qnodes = static_cast<const float4*>(p);
+        c->sc.q_ok = 1u;
+    }
     if ((rc = upload(c.get(), L.wtri.data(), L.wtri.size() * 16, &p))) return rc;
     c->sc.wtri = static_cast<const float4*>(p);
     if ((rc = upload(c.get(), L.lbox.data(), L.lbox.size() * 16, &p))) return rc;
     c->sc.lbox = static_cast<const float4*>(p);
-    if ((rc = upload(c.get(), L.bsdfs.data(), L.bsdfs.size() * sizeof(BsdfRecord), &p))) return rc;
+    {
+        const std::vector<BsdfRecord> dev_bsdfs = device_bsdfs(L.bsdfs);
+        if ((rc = upload(c.get(), dev_bsdfs.data(), dev_bsdfs.size() * sizeof(BsdfRecord), &p))) return rc;
+    }
     c->sc.bsdf = static_cast<const BsdfRecord*>(p);
     if ((rc = upload(c.get(), L.emitters.data(), L.emitters.size() * sizeof(EmitterRecord), &p))) return rc;
     c->sc.emit = static_cast<const EmitterRecord*>(p);

@@ -42,6 +42,7 @@ struct DevScene {
     const float4* __restrict__ shade;
     const float4* __restrict__ nodes;   // the reference's binary tree (2 child boxes per record)
     const float4* __restrict__ wnodes;  // 4-wide traversal nodes (wide_bvh.hpp)
+    const float4* __restrict__ qnodes;  // the same nodes compressed to 64 B (quantize_wide_nodes), or null
     const float4* __restrict__ wtri;    // traversal triangles, that tree's leaf order (v0|ref index, e1|ref leaf, e2)
     const float4* __restrict__ lbox;    // exact box of every reference leaf (lo, hi)
     const BsdfRecord* __restrict__ bsdf;
@@ -73,6 +74,7 @@ struct DevScene {
     // in o - v0), so the reference can accept a triangle the ray's line misses by
     // more than the traversal tree's padding.
     float near_lo[3], near_hi[3];
+    uint32_t q_ok;  // qnodes present: the BDPT_QNODES kernels walk the 4-wide tree (else the binary one)
 };
 constexpr uint32_t kNoLds = 0xffffffffu;
 constexpr uint32_t kLdsHdr = 4;  // LDS header words: mt_ring (2 words), mt_ring_stride, unused
@@ -505,7 +507,13 @@ struct RayInv {
     bool fast;
     float near;  // boxes left before t = near are culled (kCullNear, or -inf: no near cull, see cull_near_for)
 };
+#ifndef BDPT_QNODES
+#define BDPT_QNODES 0  // 1: the walk reads the 64-byte compressed node records (wide_bvh.hpp quantize_wide_nodes)
+#endif
 __device__ __forceinline__ bool far_origin(const DevScene& sc, f3 o) {
+#if BDPT_QNODES
+    if (!sc.q_ok) return true;  // no compressed records: every query walks the reference's tree
+#endif
     return !(o.x >= sc.near_lo[0] && o.x <= sc.near_hi[0] && o.y >= sc.near_lo[1] && o.y <= sc.near_hi[1] &&
              o.z >= sc.near_lo[2] && o.z <= sc.near_hi[2]);
 }
@@ -517,17 +525,27 @@ __device__ __forceinline__ RayInv ray_inv(const Ray& r, float near) {
     ri.inv = mk(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
     const float probe = (ri.inv.x + ri.inv.y + ri.inv.z) * 0.f + ((r.o.x + r.o.y + r.o.z) * 0.f);
     ri.fast = (probe == 0.f);  // false iff some component is +-inf or NaN
+#if BDPT_QNODES
+    // the compressed records' 2^e / d must stay normal and finite (wide_bvh.hpp kQuantExpMin/Max)
+    const float m = fmaxf(fmaxf(fabsf(ri.inv.x), fabsf(ri.inv.y)), fabsf(ri.inv.z));
+    const float n = fminf(fminf(fabsf(ri.inv.x), fabsf(ri.inv.y)), fabsf(ri.inv.z));
+    ri.fast = ri.fast && m <= 0x1p96f && n >= 0x1p-40f;
+#endif
     return ri;
+}
+__device__ __forceinline__ int slab_planes(float x0, float x1, float y0, float y1, float z0, float z1, float& tn,
+                                           float& tf) {
+    tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    const float d = tf - tn, s = fmaf(fabsf(tn) + fabsf(tf), 1e-6f, 1e-30f);
+    return d > s ? kSlabHit : (d < -s ? kSlabMiss : kSlabAmbiguous);  // inf operands: ambiguous
 }
 __device__ __forceinline__ int slab_fast(float lx, float ly, float lz, float hx, float hy, float hz, f3 o, f3 inv,
                                          float& tn, float& tf) {
     const float x0 = (lx - o.x) * inv.x, x1 = (hx - o.x) * inv.x;
     const float y0 = (ly - o.y) * inv.y, y1 = (hy - o.y) * inv.y;
     const float z0 = (lz - o.z) * inv.z, z1 = (hz - o.z) * inv.z;
-    tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-    tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-    const float d = tf - tn, s = fmaf(fabsf(tn) + fabsf(tf), 1e-6f, 1e-30f);
-    return d > s ? kSlabHit : (d < -s ? kSlabMiss : kSlabAmbiguous);  // inf operands: ambiguous
+    return slab_planes(x0, x1, y0, y1, z0, z1, tn, tf);
 }
 
 __device__ __forceinline__ int cross_le(float a, float b) {  // a <= b with the same slack
@@ -794,7 +812,7 @@ __device__ __forceinline__ int child_fast(float lx, float hx, float ly, float hy
 struct TravScene {
     const float4* __restrict__ wtri;
     const float4* __restrict__ lbox;
-    const float4* __restrict__ wnodes;
+    const float4* __restrict__ wnodes;  // the records the walk reads (qnodes in the BDPT_QNODES build)
     uint32_t wroot_link;
     uint32_t node_slack;  // 0: interior boxes tested without the ambiguity slack (DevScene::node_slack)
 };
@@ -805,7 +823,7 @@ __device__ __forceinline__ const float4* uniform_ptr(const float4* p) {
     return reinterpret_cast<const float4*>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 __device__ __forceinline__ TravScene trav_scene(const DevScene& sc) {
-    return TravScene{uniform_ptr(sc.wtri), uniform_ptr(sc.lbox), uniform_ptr(sc.wnodes),
+    return TravScene{uniform_ptr(sc.wtri), uniform_ptr(sc.lbox), uniform_ptr(BDPT_QNODES ? sc.qnodes : sc.wnodes),
                      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sc.wroot_link))),
                      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sc.node_slack)))};
 }
@@ -878,35 +896,70 @@ __device__ __forceinline__ bool trav_pop(const Ray& r, bool any, TravState& ts, 
     return false;
 }
 
+// A 4-wide node record as the walk reads it: the 128-byte float record
+// (wide_bvh.hpp; v[0..5] = lo.x hi.x lo.y hi.y lo.z hi.z, v[6] = links) or, in
+// the BDPT_QNODES build, the 64-byte compressed one (v[0] = grid origin and
+// exponents, v[1..2] = 8-bit child bounds, v[3] = links).
+#if BDPT_QNODES
+constexpr int kNodeVecs = 4, kNodeStride = 4, kNodeLinks = 3;
+#else
+constexpr int kNodeVecs = 7, kNodeStride = 8, kNodeLinks = 6;
+#endif
+struct WNode {
+    float4 v[kNodeVecs];
+};
+__device__ __forceinline__ WNode load_wnode(const float4* __restrict__ base, uint32_t link) {
+    const float4* nd = base + kNodeStride * static_cast<size_t>(link);
+    WNode n;
+#pragma unroll
+    for (int j = 0; j < kNodeVecs; j++) n.v[j] = gld4(nd + j);
+    return n;
+}
+__device__ __forceinline__ float qbyte(float w, int c) {  // byte c of the word, as a float (v_cvt_f32_ubyteN)
+    return static_cast<float>((__float_as_uint(w) >> (8 * c)) & 0xffu);
+}
+
 // Interior 4-wide node ts.link: tests the four children, descends into the
 // nearest hit child (true) and stacks the others far-to-near; false when no
 // child is hit (the caller pops).
 template <bool COUNT, bool SLACK>
-__device__ __forceinline__ bool trav_node_vals(float4 lx, float4 hx, float4 ly, float4 hy, float4 lz, float4 hz,
-                                               float4 lk, const Ray& r, const RayInv& ri, bool any, TravState& ts,
-                                               const Stack& stk, Counts& cnt);
+__device__ __forceinline__ bool trav_node_vals(const WNode& n, const Ray& r, const RayInv& ri, bool any,
+                                               TravState& ts, const Stack& stk, Counts& cnt);
 template <bool COUNT, bool SLACK>
 __device__ __forceinline__ bool trav_node(const TravScene& sc, const Ray& r, const RayInv& ri, bool any, TravState& ts,
                                           const Stack& stk, Counts& cnt) {
-    const float4* nd = sc.wnodes + 8 * static_cast<size_t>(ts.link);
-    return trav_node_vals<COUNT, SLACK>(gld4(nd), gld4(nd + 1), gld4(nd + 2), gld4(nd + 3), gld4(nd + 4),
-                                        gld4(nd + 5), gld4(nd + 6), r, ri, any, ts, stk, cnt);
+    return trav_node_vals<COUNT, SLACK>(load_wnode(sc.wnodes, ts.link), r, ri, any, ts, stk, cnt);
 }
 template <bool COUNT, bool SLACK>
-__device__ __forceinline__ bool trav_node_vals(float4 lx, float4 hx, float4 ly, float4 hy, float4 lz, float4 hz,
-                                               float4 lk, const Ray& r, const RayInv& ri, bool any, TravState& ts,
-                                               const Stack& stk, Counts& cnt) {
+__device__ __forceinline__ bool trav_node_vals(const WNode& n, const Ray& r, const RayInv& ri, bool any,
+                                               TravState& ts, const Stack& stk, Counts& cnt) {
     if (COUNT) cnt.c[2]++;
     const float far = cull_far(any ? r.max_t : ts.best_t);
+    const float4 lk = n.v[kNodeLinks];
+#if BDPT_QNODES
+    // plane distance of bound org + q 2^e: fma(q, 2^e / d, (org - o) / d); 2^e / d is exact
+    const uint32_t eb = __float_as_uint(n.v[0].w);
+    const float ax = __uint_as_float((eb & 0xffu) << 23) * ri.inv.x;
+    const float ay = __uint_as_float(((eb >> 8) & 0xffu) << 23) * ri.inv.y;
+    const float az = __uint_as_float(((eb >> 16) & 0xffu) << 23) * ri.inv.z;
+    const float bx = (n.v[0].x - r.o.x) * ri.inv.x, by = (n.v[0].y - r.o.y) * ri.inv.y,
+                bz = (n.v[0].z - r.o.z) * ri.inv.z;
+#endif
     float key[4];
     uint32_t lnk[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-        const float clx = (&lx.x)[c], chx = (&hx.x)[c], cly = (&ly.x)[c], chy = (&hy.x)[c], clz = (&lz.x)[c],
-                    chz = (&hz.x)[c];
         const uint32_t l = __float_as_uint((&lk.x)[c]);
         float tn, tf;
+#if BDPT_QNODES
+        const int d = slab_planes(fmaf(qbyte(n.v[1].x, c), ax, bx), fmaf(qbyte(n.v[1].y, c), ax, bx),
+                                  fmaf(qbyte(n.v[1].z, c), ay, by), fmaf(qbyte(n.v[1].w, c), ay, by),
+                                  fmaf(qbyte(n.v[2].x, c), az, bz), fmaf(qbyte(n.v[2].y, c), az, bz), tn, tf);
+#else
+        const float clx = (&n.v[0].x)[c], chx = (&n.v[1].x)[c], cly = (&n.v[2].x)[c], chy = (&n.v[3].x)[c],
+                    clz = (&n.v[4].x)[c], chz = (&n.v[5].x)[c];
         const int d = slab_fast(clx, cly, clz, chx, chy, chz, r.o, ri.inv, tn, tf);
+#endif
         const bool pass = SLACK ? d != kSlabMiss : !(tn > tf);
         const bool hit = l != kEmptyLinkDev && pass && !(tn > far) && !(tf < ri.near);
         key[c] = hit ? tn : __builtin_inff();
@@ -942,20 +995,21 @@ __device__ __forceinline__ bool trav_node_vals(float4 lx, float4 hx, float4 ly, 
 // the shading step, from broadcast LDS reads — instead of as the first two
 // global-memory steps of the walk loop (walk_begin_lds).
 struct RootLds {
-    float4 root[7];
-    float4 kid[4 * 7];
+    WNode root;
+    WNode kid[4];
 };
 __device__ __forceinline__ bool root_lds_usable(const DevScene& sc) { return !(sc.wroot_link & kLeafBit); }
 __device__ __forceinline__ void root_lds_fill(RootLds& m, const DevScene& sc) {
     if (!root_lds_usable(sc)) return;
-    const float4* rn = sc.wnodes + 8 * static_cast<size_t>(sc.wroot_link);
-    if (threadIdx.x < 7) {
-        m.root[threadIdx.x] = gld4(rn + threadIdx.x);
-    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + 28) {
-        const int k = (threadIdx.x - 64) / 7, j = (threadIdx.x - 64) % 7;
-        const float4 lk = gld4(rn + 6);
+    const float4* const base = BDPT_QNODES ? sc.qnodes : sc.wnodes;
+    const float4* rn = base + kNodeStride * static_cast<size_t>(sc.wroot_link);
+    if (threadIdx.x < kNodeVecs) {
+        m.root.v[threadIdx.x] = gld4(rn + threadIdx.x);
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + 4 * kNodeVecs) {
+        const int k = (threadIdx.x - 64) / kNodeVecs, j = (threadIdx.x - 64) % kNodeVecs;
+        const float4 lk = gld4(rn + kNodeLinks);
         const uint32_t l = __float_as_uint((&lk.x)[k]);
-        if (l != kEmptyLinkDev && !(l & kLeafBit)) m.kid[7 * k + j] = gld4(sc.wnodes + 8 * static_cast<size_t>(l) + j);
+        if (l != kEmptyLinkDev && !(l & kLeafBit)) m.kid[k].v[j] = gld4(base + kNodeStride * static_cast<size_t>(l) + j);
     }
 }
 // The root and (when the walk descends into an interior child) that child;
@@ -964,18 +1018,14 @@ template <bool COUNT, bool SLACK>
 __device__ __forceinline__ bool walk_begin_lds(const RootLds& m, const Ray& r, const RayInv& ri, bool any,
                                                TravState& ts, const Stack& stk, Counts& cnt) {
     if (COUNT) cnt.c[8]++;
-    bool live = trav_node_vals<COUNT, SLACK>(m.root[0], m.root[1], m.root[2], m.root[3], m.root[4], m.root[5],
-                                             m.root[6], r, ri, any, ts, stk, cnt);
+    bool live = trav_node_vals<COUNT, SLACK>(m.root, r, ri, any, ts, stk, cnt);
     if (live && !(ts.link & kLeafBit)) {
-        const float4 lk = m.root[6];
+        const float4 lk = m.root.v[kNodeLinks];
         const int k = ts.link == __float_as_uint(lk.x) ? 0
                       : ts.link == __float_as_uint(lk.y) ? 1
                       : ts.link == __float_as_uint(lk.z) ? 2 : 3;
-        const float4* kn = m.kid + 7 * k;
         if (COUNT) cnt.c[8]++;
-        live = trav_node_vals<COUNT, SLACK>(kn[0], kn[1], kn[2], kn[3], kn[4], kn[5], kn[6], r, ri, any, ts, stk,
-                                            cnt) ||
-               trav_pop(r, any, ts, stk);
+        live = trav_node_vals<COUNT, SLACK>(m.kid[k], r, ri, any, ts, stk, cnt) || trav_pop(r, any, ts, stk);
     }
     return live;
 }

@@ -847,6 +847,9 @@ bool build_device_layout(const HostScene& s, DeviceLayout& out, std::string& err
         out.wleaves = tb.bvh.leaves;
         out.wtri.swap(tb.tri);
         out.lbox.swap(tb.leaf_box);
+        // the padded boxes absorb the compressed records' slab rounding (wide_bvh.hpp)
+        out.q_ok = quantize_wide_nodes(out.wnodes, out.qnodes);
+        if (!out.q_ok) out.qnodes.clear();
     } else {
         WideBvh wb;
         if (!build_wide_bvh(s.nodes, wb, err)) return false;

@@ -73,6 +73,8 @@ struct DeviceLayout {
     std::vector<float4_t> nodes;    // 4 per interior node (the reference's binary tree)
     uint32_t root_link = 0;
     std::vector<float4_t> wnodes;   // 8 per 4-wide traversal node (wide_bvh.hpp)
+    std::vector<float4_t> qnodes;   // 4 per node: the same tree compressed (quantize_wide_nodes)
+    bool q_ok = false;              // qnodes built (triangle tree, every node on the grid)
     uint32_t wroot_link = 0;
     int wmax_stack = 0, wdepth = 0;
     int64_t wleaves = 0;

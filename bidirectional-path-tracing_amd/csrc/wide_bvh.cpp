@@ -341,4 +341,45 @@ bool build_wide_bvh_tris(const std::vector<FlatNode>& flat, const std::vector<fl
     return true;
 }
 
+bool quantize_wide_nodes(const std::vector<float4_t>& wn, std::vector<float4_t>& out) {
+    const size_t nn = wn.size() / 8;
+    out.assign(4 * nn, float4_t{0.f, 0.f, 0.f, 0.f});
+    for (size_t i = 0; i < nn; i++) {
+        const float4_t* r = &wn[8 * i];
+        uint32_t link[4];
+        std::memcpy(link, &r[6], 16);
+        float org[3];
+        uint32_t ebits = 0, qw[6] = {0, 0, 0, 0, 0, 0};  // lo.x hi.x lo.y hi.y lo.z hi.z, one byte per child
+        for (int a = 0; a < 3; a++) {
+            const float* lo = &r[2 * a].x;
+            const float* hi = &r[2 * a + 1].x;
+            float o = __builtin_inff(), top = -__builtin_inff();
+            for (int c = 0; c < 4; c++)
+                if (link[c] != kEmptyLink) o = std::min(o, lo[c]), top = std::max(top, hi[c]);
+            if (o > top) o = top = 0.f;  // no child (not built, kept well-formed)
+            if (!std::isfinite(o) || !std::isfinite(top)) return false;
+            const double ext = double(top) - double(o);
+            int e = kQuantExpMin;
+            while (ext > 255.0 * std::ldexp(1.0, e))
+                if (++e > kQuantExpMax) return false;
+            const double step = std::ldexp(1.0, e);
+            for (int c = 0; c < 4; c++) {
+                if (link[c] == kEmptyLink) continue;
+                const double ql = std::floor((double(lo[c]) - o) / step), qh = std::ceil((double(hi[c]) - o) / step);
+                if (ql < 0.0 || qh > 255.0 || ql > qh) return false;  // cannot happen: lo, hi in [o, top]
+                qw[2 * a] |= static_cast<uint32_t>(ql) << (8 * c);
+                qw[2 * a + 1] |= static_cast<uint32_t>(qh) << (8 * c);
+            }
+            org[a] = o;
+            ebits |= static_cast<uint32_t>(e + 127) << (8 * a);
+        }
+        float4_t* q = &out[4 * i];
+        q[0] = {org[0], org[1], org[2], u2f(ebits)};
+        q[1] = {u2f(qw[0]), u2f(qw[1]), u2f(qw[2]), u2f(qw[3])};
+        q[2] = {u2f(qw[4]), u2f(qw[5]), 0.f, 0.f};
+        q[3] = r[6];
+    }
+    return true;
+}
+
 }  // namespace bdpt

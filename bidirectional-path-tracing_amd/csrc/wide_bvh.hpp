@@ -74,4 +74,20 @@ struct TriWideBvh {
 bool build_wide_bvh_tris(const std::vector<FlatNode>& flat, const std::vector<float4_t>& tri,
                          const std::vector<float4_t>& shade, float pad_rel, TriWideBvh& out, std::string& err);
 
+// Compressed 64-byte node records (4 float4) of the same tree, for the
+// BDPT_QNODES=1 kernels: each child box as 8-bit offsets on a per-node,
+// per-axis grid of 2^e steps from the node's box minimum, rounded outward, so
+// the decoded box contains the exact one (the difference is computed in
+// double; its rounding, ~2^-53 of a coordinate, is far inside kTriBoxPad).
+//   q0 = (org.x, org.y, org.z, (e_x + 127) | (e_y + 127) << 8 | (e_z + 127) << 16)
+//   q1 = (lo.x bytes, hi.x bytes, lo.y bytes, hi.y bytes)   byte c = child c
+//   q2 = (lo.z bytes, hi.z bytes, 0, 0)
+//   q3 = link[4] (as in the 128-byte record)
+// A child bound is org + q * 2^e; the device forms its slab distance as
+// fma(q, 2^e / d, (org - o) / d). e is kept in [kQuantExpMin, kQuantExpMax] so
+// 2^e / d stays a normal float for |1/d| in [2^-40, 2^96] (RayInv::fast);
+// false when a node needs a larger grid (non-finite or > 2.7e8-wide boxes).
+constexpr int kQuantExpMin = -80, kQuantExpMax = 20;
+bool quantize_wide_nodes(const std::vector<float4_t>& wnodes, std::vector<float4_t>& qnodes);
+
 }  // namespace bdpt
