@@ -67,6 +67,12 @@ def algorithmic_bytes_per_sample(c: dict, samples: int, m: dict = SURVEY_BYTES) 
     return b / max(samples, 1)
 
 
+def algorithmic_write_bytes(c: dict, samples: int) -> float:
+    """Bytes per camera sample the algorithm must write: every light-vertex
+    record (64 B) and every framebuffer add (12 B: camera splats + the eye add)."""
+    return (64 * c["light_verts"] + 12 * (c["splats"] + samples)) / max(samples, 1)
+
+
 # Reference CPU cost per camera sample and thread (measured on the GPU box's host,
 # round 1) — only sizes the bounded CPU sample.
 CPU_US_PER_SAMPLE = {"caustic": 18.0, "hardlight": 5.0, "hardlight_mirror": 9.0, "cbox_low": 9.0, "synth1m": 35.0}
@@ -330,6 +336,16 @@ def main() -> None:
             roof["dram_frac"] = round(traffic / kernel_s / 1e9 / HBM_PEAK_GBPS, 5)
             roof["traffic_over_algorithmic"] = round(traffic / (bps * local_samples), 4)
             roof["traffic_source"] = pm.get("source")
+            # FETCH_SIZE's x2 (MI355X_MICROARCH.md: 128-B requests tallied at 64 B) is calibrated on
+            # wide streaming reads only; this kernel's reads are 16-B gathers, so both readings are
+            # reported: `traffic` takes the doubled one (the upper bound)
+            scale = local_samples / pm["samples_per_launch"]
+            roof["traffic_bounds"] = {
+                "fetch_x1": round((pm["fetch_size_kib_raw"] * 1024 + pm["write_bytes"]) * scale),
+                "fetch_x2": round(traffic),
+                "write": round(pm["write_bytes"] * scale),
+                "write_over_algorithmic_writes": round(pm["write_bytes"] * scale / max(
+                    1.0, algorithmic_write_bytes(cts, cst["samples"]) * local_samples), 3)}
         if deep is not None:
             roof["limiter"] = deep.get("limiter")
             for k in ("active_lane_frac", "valu_issue_frac", "wait_frac", "valu_insts_per_sample"):

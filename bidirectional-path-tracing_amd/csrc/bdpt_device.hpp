@@ -1356,6 +1356,20 @@ __device__ __forceinline__ f3 bsdf_sample(const BsdfRecord& b, f3 wo, F2 u, f3& 
 
 __device__ __forceinline__ bool is_delta(const BsdfRecord& b) { return (b.type & kTypeDelta) != 0; }
 
+// The direction v in the shading frame of normal n, for evaluating BSDF b:
+// DiffuseBSDF's eval and pdf read only the z component, dot(v, n) (to_local),
+// so a diffuse lane skips Frame(n) (a sqrt, a division and a branch); the x, y
+// it leaves at 0 are never read. BDPT_DIFFUSE_Z 0 builds every frame.
+#ifndef BDPT_DIFFUSE_Z
+#define BDPT_DIFFUSE_Z 1
+#endif
+__device__ __forceinline__ f3 local_for(const BsdfRecord& b, f3 n, f3 v) {
+#if BDPT_DIFFUSE_Z
+    if (b.kind == BSDF_DIFFUSE) return mk(0.f, 0.f, dot(v, n));
+#endif
+    return local_at(n, v);
+}
+
 // ---------------------------------------------------------------- emitters
 // Distribution1D::sample (math.h:107-111): upper_bound, then clamp.
 __device__ __forceinline__ int cdf_sample(const float* cdf, int ncdf, float u) {

@@ -453,7 +453,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const float cosAtLight = dot(e_n, dir);
         const float cosAtEye = dot(-dir, L.h.n);  // = the frame's z component (to_local)
         if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
-        const f3 wi = local_at(L.h.n, -dir);
+        const f3 wi = local_for(b, L.h.n, -dir);
 #else
         const f3 wi = local_at(L.h.n, -dir);
         const float cosAtLight = dot(e_n, dir);
@@ -495,7 +495,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         if (cosCamera <= 0.f) break;
 #if BDPT_CONN_EARLY_COS >= 3
         if (dot(-e2l, L.h.n) <= 0.f) break;  // wi.z <= 0 (the frame z component, to_local)
-        const f3 wi = local_at(L.h.n, -e2l);
+        const f3 wi = local_for(b, L.h.n, -e2l);
         const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
         const f3 f = ep.f;
         if (is_zero(f)) break;
@@ -542,8 +542,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 L.c.ci++;
                 continue;
             }
-            const f3 wiL = local_at(V.n, dir);  // Frame(n) is a pure function of n
-            const f3 wiE = local_at(L.h.n, -dir);
+            const BsdfRecord& bl = bsdf_of(sc, V.mat);
+            const f3 wiL = local_for(bl, V.n, dir);  // Frame(n) is a pure function of n
+            const f3 wiE = local_for(be, L.h.n, -dir);
 #else
             const f3 wiL = local_at(V.n, dir);  // Frame(n) is a pure function of n
             const f3 wiE = local_at(L.h.n, -dir);
@@ -552,8 +553,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 L.c.ci++;
                 continue;
             }
-#endif
             const BsdfRecord& bl = bsdf_of(sc, V.mat);
+#endif
             const EvalPdfs eL = bsdf_eval_pdfs(bl, wiL, V.wo), eE = bsdf_eval_pdfs(be, wiE, L.h.wo);
             f3 Li = eL.f * eE.f;
             Li = Li * ((V.tp * L.c.tp) * invD2);
