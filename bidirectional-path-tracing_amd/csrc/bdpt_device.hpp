@@ -1138,6 +1138,9 @@ __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]);
 #ifndef BDPT_EVAL_PDFS
 #define BDPT_EVAL_PDFS 0  // 1: connections share one powf per BSDF (measured slower: 190.8 vs 195.9)
 #endif
+#ifndef BDPT_GLASS_INLINE
+#define BDPT_GLASS_INLINE 0
+#endif
 #ifndef BDPT_SAMPLE_ATTR
 #define BDPT_SAMPLE_ATTR BDPT_NOINLINE  // the non-diffuse BSDF samplers out of line
 #endif
@@ -1262,6 +1265,30 @@ __device__ __forceinline__ float fresnel_dielectric(float eta_i, float eta_t, fl
     return (rpar * rpar + rper * rper) * 0.5f;
 }
 
+// GlassBSDF::sample (glass.h:67-108: pdf 1, no eta^2 scaling).
+__device__ __forceinline__ f3 glass_sample(const BsdfRecord& b, f3 wo, F2 u, f3& wi, float& pdf) {
+    pdf = 1.f;
+    const bool entering = wo.z > 0.f;
+    float eta_i = 1.f, eta_t = b.ior;
+    if (!entering) {
+        const float q = eta_i;
+        eta_i = eta_t;
+        eta_t = q;
+    }
+    const float eta = div_cr(eta_i, eta_t);
+    const float sin2_i = glibc_fmaxf(0.f, 1.f - wo.z * wo.z);
+    const float sin2_t = eta * eta * sin2_i;
+    float cos_t = sqrt_cr(glibc_fmaxf(0.f, 1.f - sin2_t));
+    cos_t = entering ? -cos_t : cos_t;
+    const float fr = fresnel_dielectric(eta_i, eta_t, fabsf(wo.z), fabsf(cos_t));
+    if (u.x < fr) {
+        wi = reflect_z(wo);
+        return mk(1.f, 1.f, 1.f);
+    }
+    wi = mk(eta * -wo.x, eta * -wo.y, cos_t);
+    return ld3(b.tf);
+}
+
 // BSDF::sample: sets wi, returns f*cos, writes the solid-angle pdf.
 #ifndef BDPT_SAMPLE_STRUCT
 #define BDPT_SAMPLE_STRUCT 1
@@ -1276,24 +1303,8 @@ __device__ BDPT_NOINLINE f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f
             pdf = 1.f;
             wi = reflect_z(wo);
             return mk(1.f, 1.f, 1.f);
-        case BSDF_GLASS: {  // glass.h:67-108 (pdf 1, no eta^2 scaling)
-            pdf = 1.f;
-            const bool entering = wo.z > 0.f;
-            float eta_i = 1.f, eta_t = b.ior;
-            if (!entering) { float q = eta_i; eta_i = eta_t; eta_t = q; }
-            const float eta = div_cr(eta_i, eta_t);
-            const float sin2_i = glibc_fmaxf(0.f, 1.f - wo.z * wo.z);
-            const float sin2_t = eta * eta * sin2_i;
-            float cos_t = sqrt_cr(glibc_fmaxf(0.f, 1.f - sin2_t));
-            cos_t = entering ? -cos_t : cos_t;
-            const float fr = fresnel_dielectric(eta_i, eta_t, fabsf(wo.z), fabsf(cos_t));
-            if (u.x < fr) {
-                wi = reflect_z(wo);
-                return mk(1.f, 1.f, 1.f);
-            }
-            wi = mk(eta * -wo.x, eta * -wo.y, cos_t);
-            return ld3(b.tf);
-        }
+        case BSDF_GLASS:
+            return glass_sample(b, wo, u, wi, pdf);
         case BSDF_MIXTURE: {  // mixture.h:102-151
             f3 val;
             if (u.x < b.specw) {
@@ -1351,6 +1362,9 @@ __device__ __forceinline__ f3 bsdf_sample(const BsdfRecord& b, f3 wo, F2 u, f3& 
         pdf = cosine_hemisphere_pdf(wi);
         return bsdf_eval(b, wi, wo);
     }
+#if BDPT_GLASS_INLINE
+    if (b.kind == BSDF_GLASS) return glass_sample(b, wo, u, wi, pdf);  // the common delta lobe inline
+#endif
     return bsdf_sample_call(b, wo, u, wi, pdf);
 }
 
