@@ -1139,7 +1139,7 @@ __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]);
 #define BDPT_EVAL_PDFS 0  // 1: connections share one powf per BSDF (measured slower: 190.8 vs 195.9)
 #endif
 #ifndef BDPT_GLASS_INLINE
-#define BDPT_GLASS_INLINE 0
+#define BDPT_GLASS_INLINE 1  // the delta lobes' samplers inline, the Phong-bearing ones out of line (+1.1 %)
 #endif
 #ifndef BDPT_SAMPLE_ATTR
 #define BDPT_SAMPLE_ATTR BDPT_NOINLINE  // the non-diffuse BSDF samplers out of line
@@ -1363,7 +1363,12 @@ __device__ __forceinline__ f3 bsdf_sample(const BsdfRecord& b, f3 wo, F2 u, f3& 
         return bsdf_eval(b, wi, wo);
     }
 #if BDPT_GLASS_INLINE
-    if (b.kind == BSDF_GLASS) return glass_sample(b, wo, u, wi, pdf);  // the common delta lobe inline
+    if (b.kind == BSDF_GLASS) return glass_sample(b, wo, u, wi, pdf);
+    if (b.kind == BSDF_MIRROR) {  // perfectmirror.h:49-59
+        pdf = 1.f;
+        wi = reflect_z(wo);
+        return mk(1.f, 1.f, 1.f);
+    }
 #endif
     return bsdf_sample_call(b, wo, u, wi, pdf);
 }
