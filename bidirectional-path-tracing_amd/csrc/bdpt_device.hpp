@@ -615,6 +615,25 @@ __device__ __forceinline__ bool tri_test(const float4* __restrict__ tri, uint32_
 #endif
 constexpr int kLdsStack = BDPT_LDS_STACK;
 constexpr uint32_t kEmptyLinkDev = 0xffffffffu;  // unused 4-wide child slot
+// The accesses name their address space (LDS: ds_*, HBM: global_*): through
+// the generic pointers the compiler merged the two branches into one FLAT
+// access, and every FLAT load waits for vmcnt(0) and lgkmcnt(0) together —
+// each pop then also waited for all of the wave's outstanding global loads.
+#ifndef BDPT_STACK_AS
+#define BDPT_STACK_AS 1
+#endif
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#if BDPT_STACK_AS
+typedef __attribute__((address_space(3))) u32x2 lds_uint2;
+typedef __attribute__((address_space(1))) u32x2 gbl_uint2;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(1))) uint32_t gbl_u32;
+#else
+typedef u32x2 lds_uint2;
+typedef u32x2 gbl_uint2;
+typedef uint32_t lds_u32;
+typedef uint32_t gbl_u32;
+#endif
 struct Stack {
     uint2* lds;
     int stride;
@@ -622,13 +641,14 @@ struct Stack {
     uint2* gbl;  // entry k >= nlds at gbl[(k - nlds) * nslots + slot]
     uint32_t nslots, slot;
     __device__ __forceinline__ void put(int k, uint32_t link, float tn) const {
-        const uint2 e = make_uint2(link, __float_as_uint(tn));
-        if (k < nlds) lds[k * stride] = e;
-        else gbl[static_cast<size_t>(k - nlds) * nslots + slot] = e;
+        const u32x2 e = {link, __float_as_uint(tn)};
+        if (k < nlds) ((lds_uint2*)lds)[k * stride] = e;
+        else ((gbl_uint2*)gbl)[static_cast<size_t>(k - nlds) * nslots + slot] = e;
     }
     __device__ __forceinline__ uint2 get(int k) const {
-        if (k < nlds) return lds[k * stride];
-        return gbl[static_cast<size_t>(k - nlds) * nslots + slot];
+        const u32x2 e = k < nlds ? ((const lds_uint2*)lds)[k * stride]
+                                 : ((const gbl_uint2*)gbl)[static_cast<size_t>(k - nlds) * nslots + slot];
+        return make_uint2(e.x, e.y);
     }
 };
 
@@ -641,12 +661,12 @@ struct LinkStack {
     uint32_t* gbl;  // entry k >= nlds at gbl[(k - nlds) * nslots + slot]
     uint32_t nslots, slot;
     __device__ __forceinline__ void put(int k, uint32_t link, float) const {
-        if (k < nlds) lds[k * stride] = link;
-        else gbl[static_cast<size_t>(k - nlds) * nslots + slot] = link;
+        if (k < nlds) ((lds_u32*)lds)[k * stride] = link;
+        else ((gbl_u32*)gbl)[static_cast<size_t>(k - nlds) * nslots + slot] = link;
     }
     __device__ __forceinline__ uint2 get(int k) const {
-        if (k < nlds) return make_uint2(lds[k * stride], 0u);
-        return make_uint2(gbl[static_cast<size_t>(k - nlds) * nslots + slot], 0u);
+        if (k < nlds) return make_uint2(((const lds_u32*)lds)[k * stride], 0u);
+        return make_uint2(((const gbl_u32*)gbl)[static_cast<size_t>(k - nlds) * nslots + slot], 0u);
     }
 };
 
