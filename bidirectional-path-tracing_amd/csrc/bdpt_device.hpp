@@ -1454,13 +1454,20 @@ __device__ __forceinline__ int sample_emitter(const DevScene& sc, Rng& rng, floa
     const int f = lds ? cdf_sample_lds(cdf + e.cdf_offset, e.nfaces + 1, u1)
                       : cdf_sample(cdf + e.cdf_offset, e.nfaces + 1, u1);
     const F2 uv = uniform_triangle(next2(rng));
+    // Typed loads on both sides (ds_read / global_load): through one generic
+    // pointer the compiler emitted FLAT loads, which wait for vmcnt(0) and
+    // lgkmcnt(0) together.
     float4 a, b, c, d, g;
     if (lds) {
-        const float4* q = reinterpret_cast<const float4*>(g_scene_lds + sc.lds_etri_off) + 5 * (e.face_offset + f);
-        a = q[0], b = q[1], c = q[2], d = q[3], g = q[4];
+        typedef const __attribute__((address_space(3))) v4f_t lds_v4f;
+        const lds_v4f* q = (const lds_v4f*)(g_scene_lds + sc.lds_etri_off) + 5 * (e.face_offset + f);
+        const v4f_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
+        a = make_float4(q0.x, q0.y, q0.z, q0.w), b = make_float4(q1.x, q1.y, q1.z, q1.w);
+        c = make_float4(q2.x, q2.y, q2.z, q2.w), d = make_float4(q3.x, q3.y, q3.z, q3.w);
+        g = make_float4(q4.x, q4.y, q4.z, q4.w);
     } else {
         const float4* q = sc.emit_tri + 5 * static_cast<size_t>(e.face_offset + f);
-        a = q[0], b = q[1], c = q[2], d = q[3], g = q[4];
+        a = gld4(q), b = gld4(q + 1), c = gld4(q + 2), d = gld4(q + 3), g = gld4(q + 4);
     }
     const f3 v0 = mk(a.x, a.y, a.z), v1 = mk(a.w, b.x, b.y), v2 = mk(b.z, b.w, c.x);
     const f3 n0 = mk(c.y, c.z, c.w), n1 = mk(d.x, d.y, d.z), n2 = mk(d.w, g.x, g.y);

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     break;
                 }
                 unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(work, 64ull);
+                if (lane == 0) base = gadd(work, 64ull);
                 base = __shfl(base, 0);
                 if (base >= total) {
                     exhausted = true;
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 const int n = __popcll(idle);
                 const int leader = __ffsll(static_cast<unsigned long long>(idle)) - 1;
                 unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(work, static_cast<unsigned long long>(n));
+                if (lane == leader) base = gadd(work, static_cast<unsigned long long>(n));
                 base = __shfl(base, leader);
                 if (L.state == ST_IDLE) {
                     const uint64_t s = base + __popcll(idle & ((1ull << lane) - 1ull));

@@ -262,9 +262,9 @@ __device__ __forceinline__ void splat_add(float* __restrict__ fb, int pixel, f3 
     }
 #else
     float* px = fb + 3 * static_cast<size_t>(pixel);
-    atomicAdd(px + 0, v.x);
-    atomicAdd(px + 1, v.y);
-    atomicAdd(px + 2, v.z);
+    gadd(px + 0, v.x);
+    gadd(px + 1, v.y);
+    gadd(px + 2, v.z);
 #endif
 }
 
@@ -275,9 +275,9 @@ __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __res
     if (!(fr.flags & kFlagNoEyeAccum) && (L.c.Li.x != 0.f || L.c.Li.y != 0.f || L.c.Li.z != 0.f)) {
         const float inv_spp = 1.f / static_cast<float>(fr.spp);
         float* px = fb + 3 * static_cast<size_t>(L.c.pixel);
-        atomicAdd(px + 0, L.c.Li.x * inv_spp);
-        atomicAdd(px + 1, L.c.Li.y * inv_spp);
-        atomicAdd(px + 2, L.c.Li.z * inv_spp);
+        gadd(px + 0, L.c.Li.x * inv_spp);
+        gadd(px + 1, L.c.Li.y * inv_spp);
+        gadd(px + 2, L.c.Li.z * inv_spp);
     }
     L.state = ST_IDLE;
 }
@@ -331,7 +331,7 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
     const float u = next1(L.rng);
     if (!rr_on(fr) || !(u < L.c.rr)) return false;
     if (L.c.depth >= fr.depth_cap) {
-        atomicAdd(fr.capped, 1u);
+        gadd(fr.capped, 1u);
         return false;
     }
     return true;
@@ -582,7 +582,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const bool delta = is_delta(b);
         const float rrp = rr_on(fr) ? L.c.rr : 1.f;
         if (rr_on(fr) && light && !delta && L.c.nl >= fr.lv_max) {  // the store is full: flag, end the light walk
-            atomicAdd(fr.capped, 1u);
+            gadd(fr.capped, 1u);
             L.state = ST_DEFER;
             act = A_ISSUED;
             break;
@@ -723,7 +723,7 @@ __device__ __forceinline__ void flush_counts(const Counts& cnt, unsigned long lo
     for (int i = 0; i < kCounters; i++) {
         unsigned long long v = cnt.c[i];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if ((threadIdx.x & 63) == 0 && v) atomicAdd(out + i, v);
+        if ((threadIdx.x & 63) == 0 && v) gadd(out + i, v);
     }
 }
 

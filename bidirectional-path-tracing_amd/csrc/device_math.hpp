@@ -25,6 +25,22 @@ namespace dev {
 // megakernel instead of one per call site (i-cache and register pressure).
 #define BDPT_NOINLINE __attribute__((noinline))
 
+// Relaxed agent-scope atomic adds on pointers named global (global_atomic_*):
+// HIP's atomicAdd on a generic pointer the compiler cannot place becomes a FLAT
+// atomic, which also makes the wave's next waits cover LDS (lgkmcnt) too.
+typedef __attribute__((address_space(1))) float gfloat_t;
+typedef __attribute__((address_space(1))) uint32_t gu32_t;
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+__device__ __forceinline__ void gadd(float* p, float v) {
+    __hip_atomic_fetch_add((gfloat_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t gadd(uint32_t* p, uint32_t v) {
+    return __hip_atomic_fetch_add((gu32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long gadd(unsigned long long* p, unsigned long long v) {
+    return __hip_atomic_fetch_add((gu64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------- float3
 struct f3 {
     float x, y, z;

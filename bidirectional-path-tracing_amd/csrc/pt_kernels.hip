@@ -151,12 +151,12 @@ __device__ __forceinline__ void pt_finish(PtLane& L, const PtParams& P, f3 Li) {
     } else if (Li.x != 0.f || Li.y != 0.f || Li.z != 0.f) {
         const float inv_spp = 1.f / static_cast<float>(P.fr.spp);
         float* px = P.fb + 3 * static_cast<size_t>(L.pixel);
-        atomicAdd(px + 0, Li.x * inv_spp);
-        atomicAdd(px + 1, Li.y * inv_spp);
-        atomicAdd(px + 2, Li.z * inv_spp);
+        gadd(px + 0, Li.x * inv_spp);
+        gadd(px + 1, Li.y * inv_spp);
+        gadd(px + 2, Li.z * inv_spp);
     }
-    if (L.rng.m.n > 227) atomicAdd(P.counters + 2, 1ull);  // the sample ran on the ring generator
-    if (L.rng.m.n > 624) atomicAdd(P.counters + 3, 1ull);  // ... past its first wrap
+    if (L.rng.m.n > 227) gadd(P.counters + 2, 1ull);  // the sample ran on the ring generator
+    if (L.rng.m.n > 624) gadd(P.counters + 3, 1ull);  // ... past its first wrap
     L.busy = false;
     L.q = PQ_NONE;
 }
@@ -507,7 +507,7 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
             L.i = 0;
             if (hit && !is_zero(L.f) && !emitter) {
                 if (L.depth + 1 >= S.max_levels) {  // out of level stack: flagged, the sample ends
-                    atomicAdd(P.counters + 1, 1ull);
+                    gadd(P.counters + 1, 1ull);
                     return pt_finish(L, P, zero);
                 }
                 push_level(P, slot, L);
@@ -562,7 +562,7 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
             const f3 le = emission_of(sc, vis.mat);
             if (is_zero(le)) {
                 if (L.depth + 1 >= S.max_levels) {
-                    atomicAdd(P.counters + 1, 1ull);
+                    gadd(P.counters + 1, 1ull);
                     return pt_finish(L, P, zero);
                 }
                 push_level(P, slot, L);
@@ -669,7 +669,7 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
                 const int n = __popcll(idle);
                 const int leader = __ffsll(static_cast<unsigned long long>(idle)) - 1;
                 unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(P.work, static_cast<unsigned long long>(n));
+                if (lane == leader) base = gadd(P.work, static_cast<unsigned long long>(n));
                 base = __shfl(base, leader);
                 if (!L.busy) {
                     const uint64_t s = base + __popcll(idle & ((1ull << lane) - 1ull));

@@ -9,7 +9,7 @@ cd "$(dirname "$0")/../bidirectional-path-tracing_amd"
 NAME=$1; shift
 O=lib/obj_$NAME
 mkdir -p $O
-F="--offload-arch=gfx950 ${OPT:--O3} -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I../include -Icsrc"
+F="--offload-arch=gfx950 ${OPT:--O3} -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -I../include -Icsrc"
 if [ "${ALL:-0}" = "1" ]; then TUS="bdpt_kernels bdpt_kernels_deep bdpt_kernels_hbm bdpt_kernels_rr pt_kernels sample_state kat_kernels"
 else TUS="bdpt_kernels"; fi
 EXCL=""
