@@ -1156,7 +1156,7 @@ __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]);
 #define BDPT_GLOSSY_ATTR __forceinline__  // the Phong-bearing eval / pdf (measured: inline +2 %)
 #endif
 #ifndef BDPT_EVAL_PDFS
-#define BDPT_EVAL_PDFS 0  // 1: connections share one powf per BSDF (measured slower: 190.8 vs 195.9)
+#define BDPT_EVAL_PDFS 1  // 0: eval and the two pdfs through separate calls (round 2: 195.9 vs 190.8 for 1; round 3 without SLP: 245.2 vs 250.0)
 #endif
 #ifndef BDPT_GLASS_INLINE
 #define BDPT_GLASS_INLINE 1  // the delta lobes' samplers inline, the Phong-bearing ones out of line (+1.1 %)
