@@ -389,7 +389,15 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     int rc;
     if ((rc = upload(c.get(), L.tri.data(), L.tri.size() * 16, &p))) return rc;
     c->sc.tri = static_cast<const float4*>(p);
-    if ((rc = upload(c.get(), L.shade.data(), L.shade.size() * 16, &p))) return rc;
+    {  // the device shade records (bdpt_types.h kShadeStride): the host five + v0, one line each
+        const size_t ntri = L.shade.size() / 5;
+        std::vector<float4_t> dev_shade(kShadeStride * ntri, float4_t{0.f, 0.f, 0.f, 0.f});
+        for (size_t i = 0; i < ntri; i++) {
+            for (int q = 0; q < 5; q++) dev_shade[kShadeStride * i + q] = L.shade[5 * i + q];
+            if (kShadeStride > kShadeV0) dev_shade[kShadeStride * i + kShadeV0] = L.tri[3 * i];
+        }
+        if ((rc = upload(c.get(), dev_shade.data(), dev_shade.size() * 16, &p))) return rc;
+    }
     c->sc.shade = static_cast<const float4*>(p);
     if ((rc = upload(c.get(), L.nodes.data(), L.nodes.size() * 16, &p))) return rc;
     c->sc.nodes = static_cast<const float4*>(p);

@@ -1127,8 +1127,9 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool a
 
 // AcceleratorBVH::intersect's shading of a closest hit (accel.h:133-166).
 __device__ __forceinline__ void shade_hit(const DevScene& sc, int i, float u, float v, float t, f3 dir, Hit& h) {
-    const float4* sh = sc.shade + 5 * static_cast<size_t>(i);
-    const f3 v0 = xyz(gld4(sc.tri + 3 * i)), v1 = xyz(gld4(sh + 3)), v2 = xyz(gld4(sh + 4));
+    const float4* sh = sc.shade + kShadeStride * static_cast<size_t>(i);
+    const f3 v0 = xyz(gld4(BDPT_SHADE_WIDE ? sh + kShadeV0 : sc.tri + 3 * static_cast<size_t>(i))),
+             v1 = xyz(gld4(sh + 3)), v2 = xyz(gld4(sh + 4));
     const float4 s0 = gld4(sh), s1 = gld4(sh + 1), s2 = gld4(sh + 2);
     const float w = 1 - u - v;
     h.p = (v0 * w + v1 * u) + v2 * v;

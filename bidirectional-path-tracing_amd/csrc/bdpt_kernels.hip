@@ -28,6 +28,10 @@
 #endif
 #endif
 
+// The eye-estimate slots (bdpt_path.hpp) are claimed with the 64-sample chunks.
+#if defined(BDPT_SEED_CHUNK) && !BDPT_SEED_CHUNK && !defined(BDPT_EYE_SLOTS)
+#define BDPT_EYE_SLOTS 0
+#endif
 #include "bdpt_path.hpp"
 
 namespace bdpt {
@@ -120,6 +124,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     int chunk_pos = 0, chunk_n = 0;
     bool global_done = false;
     uint32_t chunk_x397 = 0;  // lane i: mt_x397 of sample chunk_base + i
+#if BDPT_EYE_SLOTS
+    static_assert(kBlock == 64 * kEyeSlotWaves, "one eye-slot row per wave");
+    uint32_t chunk_seq = 0;  // wave-uniform: chunks claimed so far (their eye slot: seq mod BDPT_EYE_SLOTS)
+    if (lane == 0)
+        for (int k = 0; k < BDPT_EYE_SLOTS; k++) wave_eye_slots()[k] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+#endif
 #endif
 #if BDPT_OVERLAP
     const TravScene tsc = trav_scene(kp.sc);
@@ -164,6 +174,13 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 global_done = base + 64 >= total;
                 int px;
                 chunk_x397 = mt_x397(sample_seed(base + lane, P->fr, px));
+#if BDPT_EYE_SLOTS
+                // the chunk's pixel when all 64 samples share one (spp a multiple of 64)
+                const int cpx = __shfl(px, 0);
+                if (lane == 0)
+                    eye_slot_reset(P->fb, static_cast<int>(chunk_seq % BDPT_EYE_SLOTS), P->fr.spp % 64 == 0 ? cpx : -1);
+                chunk_seq++;
+#endif
             }
             const int m = min(__popcll(idle), chunk_n - chunk_pos);
             const int rank = __popcll(idle & ((1ull << lane) - 1ull));
@@ -269,6 +286,10 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         if (L.state != ST_IDLE) step<FULL, COUNT>(L, P->sc, P->fr, P->fb, ls, stk, cnt);
 #endif
     }
+#if BDPT_SEED_CHUNK && BDPT_EYE_SLOTS
+    if (lane == 0)  // every sample of the wave has finished: the slots' sums to the framebuffer
+        for (int k = 0; k < BDPT_EYE_SLOTS; k++) eye_slot_reset(kp.fb, k, -1);
+#endif
     if (COUNT) {
         if (lane == 0) cnt.c[14] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - clock0);
         flush_counts(cnt, kp.counters);

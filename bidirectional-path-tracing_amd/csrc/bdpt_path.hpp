@@ -268,16 +268,63 @@ __device__ __forceinline__ void splat_add(float* __restrict__ fb, int pixel, f3 
 #endif
 }
 
+// Eye-estimate sums per wave (frame kernels). With spp a multiple of 64 the
+// megakernel's 64-sample refill chunks each cover ONE pixel, and the samples a
+// wave runs at a time come from its few most recent chunks. Each wave keeps a
+// sum (x, y, z, pixel bits in w) for each of its last BDPT_EYE_SLOTS chunks in
+// LDS: a finishing sample whose pixel has a slot adds to it (ds_add_f32) and
+// the slot goes to the framebuffer once, when its chunk's place is reused or
+// the kernel ends; any other sample adds to the framebuffer directly. The sums
+// are the same products in another order (float reassociation, as the device
+// atomics already are); each framebuffer add is a memory-side request of its
+// own, so ~3 of the ~9 per sample become ~3 per 64 samples.
+#ifndef BDPT_EYE_SLOTS
+#define BDPT_EYE_SLOTS 4
+#endif
+#if BDPT_EYE_SLOTS && !BDPT_SAMPLER_STATE
+constexpr int kEyeSlotWaves = 4;  // waves per 256-lane frame-kernel block
+__shared__ float4 eye_slots[kEyeSlotWaves][BDPT_EYE_SLOTS];
+__device__ __forceinline__ float4* wave_eye_slots() { return eye_slots[(threadIdx.x >> 6) & (kEyeSlotWaves - 1)]; }
+// Lane 0 of the wave: slot k to the framebuffer, then reset to `pixel` (-1: unused).
+__device__ __forceinline__ void eye_slot_reset(float* __restrict__ fb, int k, int pixel) {
+    float4* const s = wave_eye_slots();
+    const float4 e = s[k];
+    const int p = __float_as_int(e.w);
+    if (p >= 0 && (e.x != 0.f || e.y != 0.f || e.z != 0.f)) {
+        float* px = fb + 3 * static_cast<size_t>(p);
+        gadd(px + 0, e.x);
+        gadd(px + 1, e.y);
+        gadd(px + 2, e.z);
+    }
+    s[k] = make_float4(0.f, 0.f, 0.f, __int_as_float(pixel));
+}
+#endif
+
 template <bool COUNT>
 __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __restrict__ fb, Counts& cnt) {
     if (COUNT) cnt.c[7] += L.rng.n;
     // rgb[p] += acc * (1 / spp) (renderer.cpp:202), one sample at a time.
     if (!(fr.flags & kFlagNoEyeAccum) && (L.c.Li.x != 0.f || L.c.Li.y != 0.f || L.c.Li.z != 0.f)) {
         const float inv_spp = 1.f / static_cast<float>(fr.spp);
-        float* px = fb + 3 * static_cast<size_t>(L.c.pixel);
-        gadd(px + 0, L.c.Li.x * inv_spp);
-        gadd(px + 1, L.c.Li.y * inv_spp);
-        gadd(px + 2, L.c.Li.z * inv_spp);
+        const f3 add = L.c.Li * inv_spp;
+#if BDPT_EYE_SLOTS && !BDPT_SAMPLER_STATE
+        float4* const s = wave_eye_slots();
+        int k = -1;
+#pragma unroll
+        for (int j = 0; j < BDPT_EYE_SLOTS; j++)
+            if (__float_as_int(s[j].w) == L.c.pixel) k = j;
+        if (k >= 0) {
+            atomicAdd(&s[k].x, add.x);
+            atomicAdd(&s[k].y, add.y);
+            atomicAdd(&s[k].z, add.z);
+        } else
+#endif
+        {
+            float* px = fb + 3 * static_cast<size_t>(L.c.pixel);
+            gadd(px + 0, add.x);
+            gadd(px + 1, add.y);
+            gadd(px + 2, add.z);
+        }
     }
     L.state = ST_IDLE;
 }
@@ -345,7 +392,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
     BDPT_ACTION(21, act == A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
         const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
         if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
-            const int mat = __float_as_int(gld4(sc.shade + 5 * static_cast<size_t>(L.c.prim_tri)).w);
+            const int mat = __float_as_int(gld4(sc.shade + kShadeStride * static_cast<size_t>(L.c.prim_tri)).w);
             L.c.Li = ld3(bsdf_of(sc, mat).emission);
             act = A_FINISH;
             break;

@@ -6,6 +6,8 @@
 //   shade[5*i + c] c=0..2: (n_c.x, n_c.y, n_c.z, id_c)       id_0 = matID, id_1 = shapeID,
 //                                                            id_2 = primID (int bits)
 //                  c=3,4: (v1, 0), (v2, 0)                   for the hit point of a closest hit
+//     (host layout; the device copy has kShadeStride float4 per triangle: the
+//      same five, then (v0, 0) and padding — one 128-byte line per closest hit)
 //   nodes[4*j + q] interior node j (2-wide, both child boxes inline):
 //       q0 = c0.min.xyz, c0.max.x   q1 = c0.max.yz, c1.min.xy
 //       q2 = c1.min.z, c1.max.xyz   q3 = (link0, link1, 0, 0) as uint bits
@@ -62,6 +64,16 @@ struct CameraConstants {
     float fwd[3];
     float vnear;
 };
+
+// Device shade records: 8 float4 (128 B, line aligned) holding the host record's
+// five plus v0 at slot 5, so shading a closest hit reads one cache line instead
+// of the 80-byte record (often split over two lines) and v0 from the tri array;
+// 5 = the host layout uploaded as is.
+#ifndef BDPT_SHADE_WIDE
+#define BDPT_SHADE_WIDE 1
+#endif
+constexpr int kShadeStride = BDPT_SHADE_WIDE ? 8 : 5;
+constexpr int kShadeV0 = 5;  // slot of (v0, 0) in a wide record
 
 constexpr uint32_t kLeafBit = 0x80000000u;
 inline uint32_t make_leaf_link(uint32_t start, uint32_t count) { return kLeafBit | (start << 3) | count; }

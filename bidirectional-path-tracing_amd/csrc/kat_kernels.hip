@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, i
     if (!hit) return;
     Hit h;
     shade_hit(sc, res, u, v, t, ray.d, h);
-    const float4* sh = sc.shade + 5 * static_cast<size_t>(res);
+    const float4* sh = sc.shade + kShadeStride * static_cast<size_t>(res);
     const f3 v0 = xyz(gld4(sc.tri + 3 * static_cast<size_t>(res))), v1 = xyz(gld4(sh + 3)), v2 = xyz(gld4(sh + 4));
     const f3 ng = normalize(cross(v1 - v0, v2 - v0));
     o[0] = __int_as_float(1), o[2] = u, o[3] = v;
