@@ -89,11 +89,13 @@ DIRECT_FRAMEBUFFERS = {
                                                                          bsdf_samples=1)),
 }
 
-# BASELINE configs[3] / [4] at their full size: the reference renders a two-row
+# BASELINE configs[1] / [3] / [4] at their full size: the reference renders a few-row
 # shard (8 threads); the fixture keeps the shard's own rows (eye estimates plus the
 # splats that land on them) and block sums of the whole frame (every splat).
 # name: (scene, W, H, spp, rrDepth, row_offset, row_stride, block)
 LARGE_FRAMEBUFFERS = {
+    # the bench workload (BASELINE configs[1], the metric's frame) at its own spp: eight rows
+    "L0_caustic_512x512_spp256_rows8": ("caustic", 512, 512, 256, 8, 31, 64, 32),
     "L1_caustic_1024x1024_spp1024_rows2": ("caustic", 1024, 1024, 1024, 8, 300, 512, 32),
     "L2_synth1m_2048x2048_spp512_rows2": ("synth1m", 2048, 2048, 512, 8, 700, 1024, 64),
 }

@@ -1,5 +1,6 @@
-"""BASELINE.json configs[3] and [4] at their full size on one GPU.
+"""BASELINE.json configs[1], [3] and [4] at their full size on one GPU.
 
+* configs[1]: CausticSample 512x512, 256 spp (the bench workload; 67.1 M camera samples)
 * configs[3]: CausticSample 1024x1024, 1024 spp (1.07 G camera samples)
 * configs[4]: synthetic 1M-triangle scene, 2048x2048, 512 spp (2.15 G samples)
 
@@ -24,7 +25,7 @@ import variants
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-4
-LARGE = ["L1_caustic_1024x1024_spp1024_rows2", "L2_synth1m_2048x2048_spp512_rows2"]
+LARGE = ["L0_caustic_512x512_spp256_rows8", "L1_caustic_1024x1024_spp1024_rows2", "L2_synth1m_2048x2048_spp512_rows2"]
 _scenes = {}
 
 
