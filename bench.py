@@ -322,7 +322,7 @@ def main() -> None:
         traffic = pm["hbm_bytes_per_launch"] * local_samples / pm["samples_per_launch"] if pm else None
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
-                "kernel": "bdpt_frame_kernel",
+                "kernel": cst.get("kernel") or "bdpt_frame_kernel",
                 "kernel_build": build, "schedule": "megakernel", "kernel_ms": round(avg_kernel_ms, 3),
                 "samples_per_launch": local_samples,
                 "byte_model": "SURVEY.md 8(d): 64 B/node visit, 36 B/triangle test, 40 B/closest hit, "

@@ -172,7 +172,7 @@ class _Stats(ctypes.Structure):
 
 # Sources that make up the frame kernels' code objects: their hash stamps the
 # profiles (PMC passes) so bench.py only reuses a measurement of the same kernel.
-KERNEL_SOURCES = ("csrc/bdpt_kernels.hip", "csrc/bdpt_path.hpp", "csrc/bdpt_device.hpp", "csrc/device_math.hpp",
+KERNEL_SOURCES = ("csrc/bdpt_kernels.hip", "csrc/bdpt_kernels_split.hip", "csrc/bdpt_path.hpp", "csrc/bdpt_device.hpp", "csrc/device_math.hpp",
                   "csrc/bdpt_types.h", "Makefile")
 
 
@@ -206,6 +206,8 @@ def lib():
         vp, i32, f32p = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_float)
         L.bdpt_last_error.restype = ctypes.c_char_p
         L.bdpt_version.restype = ctypes.c_char_p
+        L.bdpt_last_kernel.restype = ctypes.c_char_p
+        L.bdpt_last_kernel.argtypes = [ctypes.c_void_p]
         L.bdpt_scene_load_obj.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
         L.bdpt_scene_free.argtypes = [vp]
         L.bdpt_scene_get_info.argtypes = [vp, ctypes.POINTER(_SceneInfo)]
@@ -709,7 +711,8 @@ class BDPTIntegrator:
         s = _Stats()
         _check(lib().bdpt_get_stats(self._h, ctypes.byref(s)))
         return dict(kernel_ms=s.kernel_ms, samples=s.samples, launches=s.launches,
-                    counters=dict(zip(COUNTER_NAMES, list(s.counters))), capped_samples=s.capped_samples)
+                    counters=dict(zip(COUNTER_NAMES, list(s.counters))), capped_samples=s.capped_samples,
+                    kernel=(lib().bdpt_last_kernel(self._h) or b"").decode())
 
     def synchronize(self) -> None:
         _check(lib().bdpt_synchronize(self._h))

@@ -55,6 +55,11 @@ hipError_t launch_frame_rr(const dev::DevScene& sc, const dev::DevFrame& fr, flo
                            uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
                            hipStream_t stream, void* dparams);
 int frame_kernel_blocks_per_cu_rr(size_t dyn_lds);
+// bdpt_kernels_split.hip: the same megakernel for short subpaths (no ST_DEFER step)
+hipError_t launch_frame_split(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf,
+                              uint2* gstack, uint32_t nslots, unsigned long long* work, unsigned long long* counters,
+                              int grid, hipStream_t stream, void* dparams);
+int frame_kernel_blocks_per_cu_split(size_t dyn_lds);
 size_t pt_params_bytes();
 int pt_blocks_per_cu(size_t dyn_lds);
 hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8], float* fb,
@@ -82,6 +87,17 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
+// Short subpaths run the BDPT_SPLIT_CONTINUE build (bdpt_kernels_split.hip): the
+// ST_DEFER step it removes is one loop slot of the ~(rrDepth + 1)^2 / 2 a sample
+// takes, while its separate light / eye continuation bodies cost every shading
+// step (measured, DESIGN.md §5: Caustic rrDepth 2 / 3 / 4 / 8: +11.4 / +1.1 / -1.5 / -3.7 %,
+// HardLight rrDepth 2 / 3 / 4 / 5: +12.5 / +4.4 / +1.2 / -0.2 %).
+// BDPT_SPLIT_MAX_RR overrides the threshold (0: never).
+constexpr int kSplitMaxRrDepth = 3;
+static bool use_split_build(int rr_depth) {
+    const char* e = std::getenv("BDPT_SPLIT_MAX_RR");  // read per render (tests force either build)
+    return rr_depth <= (e ? std::atoi(e) : kSplitMaxRrDepth);
+}
 constexpr int kMaxRrDepth = 1024;  // beyond 28 the megakernel continues MT19937 from an HBM ring
 // Russian roulette (NO_RR = 0): subpaths are unbounded in the reference (a light
 // subpath trapped by total internal reflection in the Caustic sphere was measured
@@ -118,6 +134,7 @@ struct bdpt_scene {
 };
 
 struct bdpt_ctx {
+    const char* last_kernel = "";  // the frame kernel build the last render launched (bdpt_last_kernel)
     int device = 0;
     int cus = 0;
     int grid = 0;
@@ -610,17 +627,27 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
                                                            4 * static_cast<size_t>(c->sc.lds_words)));
             HIP_TRY(launch_frame_rr(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
                                     c->dparams));
+            c->last_kernel = "bdpt_frame_kernel_rr";
         } else if (p->rr_depth > kLazyRrDepth) {  // never more resident blocks than the slots allocated
             const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_deep(
                                                            4 * static_cast<size_t>(c->sc.lds_words)));
             HIP_TRY(launch_frame_deep(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
                                       c->dparams));
+            c->last_kernel = "bdpt_frame_kernel_deep";
         } else if (hbm) {
             HIP_TRY(launch_frame_hbm(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
                                      c->dparams));
+            c->last_kernel = "bdpt_frame_kernel_hbm";
+        } else if (use_split_build(p->rr_depth)) {  // never more resident blocks than the slots allocated
+            const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_split(
+                                                           4 * static_cast<size_t>(c->sc.lds_words)));
+            HIP_TRY(launch_frame_split(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
+                                       c->dparams));
+            c->last_kernel = "bdpt_frame_kernel_split";
         } else {
             HIP_TRY(launch_frame(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
                                  c->dparams));
+            c->last_kernel = "bdpt_frame_kernel";
         }
         launches = 1;
     }
@@ -914,6 +941,8 @@ int bdpt_debug_math(int32_t device, int32_t fn, const float* x, const float* y, 
     if (e != hipSuccess) return fail(BDPT_ERR_HIP, std::string("bdpt_debug_math: ") + hipGetErrorString(e));
     return BDPT_OK;
 }
+
+const char* bdpt_last_kernel(const bdpt_ctx* c) { return c ? c->last_kernel : ""; }
 
 int bdpt_get_stats(bdpt_ctx* c, bdpt_stats* out) {
     if (!c || !out) return fail(BDPT_ERR_INVALID, "null argument");

@@ -384,11 +384,109 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
     return true;
 }
 
+#ifndef BDPT_SPLIT_CONTINUE
+#define BDPT_SPLIT_CONTINUE 0  // 1: the light subpath's continuation runs before the eye subpath's start, so a light walk that ends starts its eye walk in the same sweep (no ST_DEFER step); the eye continuation is its own body
+#endif
+/* Bodies placed at two points of the sweep (BDPT_SPLIT_CONTINUE). */
+#define BDPT_BODY_LIGHT_VERTEX \
+    BDPT_ACTION(26, act == A_LIGHT_VERTEX) {  /* bdpt.h:193-209 */ \
+        const float dist2 = L.h.dist * L.h.dist; \
+        const float absCosIn = fabsf(L.h.wo.z); \
+        L.c.vcm *= div_cr(dist2, absCosIn); \
+        L.c.vc *= rcp_cr(absCosIn); \
+        act = A_LIGHT_CONTINUE; \
+        if (rr_on(fr)) L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);  /* bdpt.h:201-204 */ \
+        const BsdfRecord& b = bsdf_of(sc, L.h.mat); \
+        if (is_delta(b)) break; \
+        /* connectToCamera (bdpt.h:295-371): everything but the visibility test. */ \
+        f3 e2l = L.h.p - cam_o; \
+        const float invD2 = rcp_cr(dot(e2l, e2l)); \
+        e2l = e2l * sqrt_cr(invD2); \
+        int xp, yp; \
+        splat_pixel(fr.cam, L.h.p, xp, yp); \
+        if (xp < 0 || yp < 0 || xp >= fr.W || yp >= fr.H) break; \
+        const float cosCamera = dot(fwd, e2l); \
+        if (cosCamera <= 0.f) break; \
+        const bool early_cos_ = BDPT_CONN_EARLY_COS >= 3; /* reject on wi.z = dot(-e2l, n) (the frame z component, to_local) first */ \
+        if (early_cos_ && dot(-e2l, L.h.n) <= 0.f) break; \
+        const f3 wi = early_cos_ ? local_for(b, L.h.n, -e2l) : local_at(L.h.n, -e2l); \
+        const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo); \
+        const f3 f = ep.f; \
+        if (is_zero(f) || (!early_cos_ && wi.z <= 0.f)) break; \
+        const float d = div_cr(fr.cam.vnear, cosCamera); \
+        const float img2solid = div_cr(d * d, cosCamera); \
+        const float img2surf = img2solid * (wi.z * invD2); \
+        const float surf2img = rcp_cr(img2surf); \
+        const float nlight = static_cast<float>(fr.W * fr.H); \
+        f3 rad = L.c.tp * (f * rcp_cr(wi.z)); \
+        rad = rad * rcp_cr(surf2img); \
+        rad = rad * rcp_cr(nlight); \
+        rad = rad * rcp_cr(static_cast<float>(fr.spp)); \
+        const float reversePdf_a = 1.f * img2surf; \
+        const float prevRev = ep.rev * (rr_on(fr) ? L.c.rr : 1.f);  /* swapped (wi, wo) * lightVertex.rr (bdpt.h:342) */ \
+        const float lightWeight = div_cr(reversePdf_a, nlight) * (L.c.vcm + prevRev * L.c.vc); \
+        const float mis = rcp_cr(lightWeight + 1.f + 0.f); \
+        L.c.pend = (fr.strategy == 0) ? rad * mis : rad; \
+        L.c.pend_px = yp * fr.W + xp; \
+        L.ray = shadow_ray(cam_o, L.h.p); \
+        L.state = ST_SPLAT; \
+        act = A_ISSUED; \
+    } BDPT_END;
+#define BDPT_BODY_CONTINUE(ACT_, COND_) \
+    /* ContinuePathRandomWalk of either subpath (light: bdpt.h:211-215, eye: bdpt.h:152). */ \
+    BDPT_ACTION(28, COND_) { \
+        const bool light = act == A_LIGHT_CONTINUE; \
+        const BsdfRecord& b = bsdf_of(sc, L.h.mat); \
+        const bool delta = is_delta(b); \
+        const float rrp = rr_on(fr) ? L.c.rr : 1.f; \
+        if (rr_on(fr) && light && !delta && L.c.nl >= fr.lv_max) {  /* the store is full: flag, end the light walk */ \
+            gadd(fr.capped, 1u); \
+            L.state = ST_DEFER; \
+            act = A_ISSUED; \
+            break; \
+        } \
+        if (light && !delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, rrp);  /* the pre-walk state */ \
+        const bool more = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, rrp); \
+        if (!light) { \
+            act = more ? A_EYE_NEXT : A_FINISH; \
+        } else if (more) { \
+            if (!delta) { \
+                L.c.nl++; \
+                if (COUNT) cnt.c[4]++; \
+            } \
+            act = A_LIGHT_NEXT; \
+        } else if (BDPT_SPLIT_CONTINUE) {  /* the light subpath ends; the eye subpath starts in this sweep */ \
+            act = A_START_EYE; \
+        } else {  /* the light subpath ends; the eye subpath starts next step */ \
+            L.state = ST_DEFER; \
+            act = A_ISSUED; \
+        } \
+    } BDPT_END;
+#define BDPT_BODY_LIGHT_NEXT \
+    /* Loop conditions `depth < m_rrDepth || (sampler.next() < rrProbability && !NO_RR)` */ \
+    /* (bdpt.h:188, :68): past rrDepth one draw, then (RR only) a continuation. */ \
+    BDPT_ACTION(29, act == A_LIGHT_NEXT) { \
+        if (walk_continues(L, fr)) { \
+            L.state = ST_LIGHT; \
+            act = A_ISSUED; \
+        } else if (BDPT_SPLIT_CONTINUE) { \
+            act = A_START_EYE;  /* the eye subpath starts in this sweep */ \
+        } else { \
+            L.state = ST_DEFER;  /* the eye subpath starts next step */ \
+            act = A_ISSUED; \
+        } \
+    } BDPT_END;
+
 template <bool COUNT>
 __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
                         const LightStore& ls, Counts& cnt) {
     const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
     const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
+#if BDPT_SPLIT_CONTINUE
+    BDPT_BODY_LIGHT_VERTEX
+    BDPT_BODY_CONTINUE(A_LIGHT_CONTINUE, act == A_LIGHT_CONTINUE)
+    BDPT_BODY_LIGHT_NEXT
+#endif
     BDPT_ACTION(21, act == A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
         const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
         if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
@@ -485,6 +583,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         if (edir.z <= 0.f) {  // bdpt.h:179-182 (the eye subpath follows)
             L.state = ST_DEFER;
             act = A_ISSUED;
+        } else if (BDPT_SPLIT_CONTINUE) {  // the loop test of bdpt.h:188 here: its body runs earlier in the sweep
+            L.state = walk_continues(L, fr) ? ST_LIGHT : ST_DEFER;
+            act = A_ISSUED;
         } else {
             act = A_LIGHT_NEXT;
         }
@@ -522,55 +623,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         L.state = ST_NEE;
         act = A_ISSUED;
     } BDPT_END;
-    BDPT_ACTION(26, act == A_LIGHT_VERTEX) {  // bdpt.h:193-209
-        const float dist2 = L.h.dist * L.h.dist;
-        const float absCosIn = fabsf(L.h.wo.z);
-        L.c.vcm *= div_cr(dist2, absCosIn);
-        L.c.vc *= rcp_cr(absCosIn);
-        act = A_LIGHT_CONTINUE;
-        if (rr_on(fr)) L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);  // bdpt.h:201-204
-        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
-        if (is_delta(b)) break;
-        // connectToCamera (bdpt.h:295-371): everything but the visibility test.
-        f3 e2l = L.h.p - cam_o;
-        const float invD2 = rcp_cr(dot(e2l, e2l));
-        e2l = e2l * sqrt_cr(invD2);
-        int xp, yp;
-        splat_pixel(fr.cam, L.h.p, xp, yp);
-        if (xp < 0 || yp < 0 || xp >= fr.W || yp >= fr.H) break;
-        const float cosCamera = dot(fwd, e2l);
-        if (cosCamera <= 0.f) break;
-#if BDPT_CONN_EARLY_COS >= 3
-        if (dot(-e2l, L.h.n) <= 0.f) break;  // wi.z <= 0 (the frame z component, to_local)
-        const f3 wi = local_for(b, L.h.n, -e2l);
-        const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
-        const f3 f = ep.f;
-        if (is_zero(f)) break;
-#else
-        const f3 wi = local_at(L.h.n, -e2l);
-        const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
-        const f3 f = ep.f;
-        if (is_zero(f) || wi.z <= 0.f) break;
+#if !BDPT_SPLIT_CONTINUE
+    BDPT_BODY_LIGHT_VERTEX
 #endif
-        const float d = div_cr(fr.cam.vnear, cosCamera);
-        const float img2solid = div_cr(d * d, cosCamera);
-        const float img2surf = img2solid * (wi.z * invD2);
-        const float surf2img = rcp_cr(img2surf);
-        const float nlight = static_cast<float>(fr.W * fr.H);
-        f3 rad = L.c.tp * (f * rcp_cr(wi.z));
-        rad = rad * rcp_cr(surf2img);
-        rad = rad * rcp_cr(nlight);
-        rad = rad * rcp_cr(static_cast<float>(fr.spp));
-        const float reversePdf_a = 1.f * img2surf;
-        const float prevRev = ep.rev * (rr_on(fr) ? L.c.rr : 1.f);  // swapped (wi, wo) * lightVertex.rr (bdpt.h:342)
-        const float lightWeight = div_cr(reversePdf_a, nlight) * (L.c.vcm + prevRev * L.c.vc);
-        const float mis = rcp_cr(lightWeight + 1.f + 0.f);
-        L.c.pend = (fr.strategy == 0) ? rad * mis : rad;
-        L.c.pend_px = yp * fr.W + xp;
-        L.ray = shadow_ray(cam_o, L.h.p);
-        L.state = ST_SPLAT;
-        act = A_ISSUED;
-    } BDPT_END;
     BDPT_ACTION(27, act == A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
         act = A_EYE_CONTINUE;
         if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
@@ -622,39 +677,12 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             break;
         }
     } BDPT_END;
-    // ContinuePathRandomWalk of either subpath (light: bdpt.h:211-215, eye: bdpt.h:152).
-    BDPT_ACTION(28, act == A_LIGHT_CONTINUE || act == A_EYE_CONTINUE) {
-        const bool light = act == A_LIGHT_CONTINUE;
-        const BsdfRecord& b = bsdf_of(sc, L.h.mat);
-        const bool delta = is_delta(b);
-        const float rrp = rr_on(fr) ? L.c.rr : 1.f;
-        if (rr_on(fr) && light && !delta && L.c.nl >= fr.lv_max) {  // the store is full: flag, end the light walk
-            gadd(fr.capped, 1u);
-            L.state = ST_DEFER;
-            act = A_ISSUED;
-            break;
-        }
-        if (light && !delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, rrp);  // the pre-walk state
-        const bool more = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, rrp);
-        if (!light) {
-            act = more ? A_EYE_NEXT : A_FINISH;
-        } else if (more) {
-            if (!delta) {
-                L.c.nl++;
-                if (COUNT) cnt.c[4]++;
-            }
-            act = A_LIGHT_NEXT;
-        } else {  // the light subpath ends; the eye subpath starts next step
-            L.state = ST_DEFER;
-            act = A_ISSUED;
-        }
-    } BDPT_END;
-    // Loop conditions `depth < m_rrDepth || (sampler.next() < rrProbability && !NO_RR)`
-    // (bdpt.h:188, :68): past rrDepth one draw, then (RR only) a continuation.
-    BDPT_ACTION(29, act == A_LIGHT_NEXT) {
-        L.state = walk_continues(L, fr) ? ST_LIGHT : ST_DEFER;  // ST_DEFER: the eye subpath starts next step
-        act = A_ISSUED;
-    } BDPT_END;
+#if BDPT_SPLIT_CONTINUE
+    BDPT_BODY_CONTINUE(A_EYE_CONTINUE, act == A_EYE_CONTINUE)
+#else
+    BDPT_BODY_CONTINUE(A_LIGHT_CONTINUE, act == A_LIGHT_CONTINUE || act == A_EYE_CONTINUE)
+    BDPT_BODY_LIGHT_NEXT
+#endif
     BDPT_ACTION(30, act == A_EYE_NEXT) {
         if (walk_continues(L, fr)) {
             L.state = ST_EYE;
@@ -670,6 +698,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
 }
 #undef BDPT_ACTION
 #undef BDPT_END
+#undef BDPT_BODY_LIGHT_VERTEX
+#undef BDPT_BODY_CONTINUE
+#undef BDPT_BODY_LIGHT_NEXT
 
 // Pixel and Sampler seed of sample `s` of the shard: seed_base + p * spp + k
 // (the per-(pixel, sample) convention of SURVEY §8c on renderer.cpp:155).

@@ -263,6 +263,11 @@ int bdpt_render_sample_mt(bdpt_ctx* ctx, const bdpt_frame_params* params, const 
 int bdpt_render_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, const float ray[8], uint32_t sampler_seed,
                        int32_t* sampler_draws, float Li[3], float* fb_host);
 int bdpt_get_stats(bdpt_ctx* ctx, bdpt_stats* out);
+/* (new) The frame-kernel build the context's last bdpt_render launched: "bdpt_frame_kernel",
+ * "_split" (rrDepth <= 3: no deferred shading step between the subpaths), "_deep" (rrDepth > 28),
+ * "_rr" (Russian roulette) or "_hbm" (BSDF records in HBM); "" before the first render. For
+ * matching profiler records to the kernel that ran. */
+const char* bdpt_last_kernel(const bdpt_ctx* ctx);
 /* Waits for all work queued by this context (on every stream it was given). */
 int bdpt_synchronize(bdpt_ctx* ctx);
 

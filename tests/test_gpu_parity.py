@@ -668,3 +668,18 @@ def test_gpu_russian_roulette_limits():
     it.config.russian_roulette = 7
     with pytest.raises(bdpt_amd.BdptError, match="russian_roulette"):
         it.render_frame()
+
+
+# Both frame-kernel builds on every BDPT golden: the default sweep order and the
+# short-subpath build (BDPT_SPLIT_CONTINUE, bdpt_kernels_split.hip; chosen per render
+# for rrDepth <= 3), forced through BDPT_SPLIT_MAX_RR, which the library reads per render.
+@pytest.mark.parametrize("build,max_rr", [("default", "0"), ("split", "1024")])
+@pytest.mark.parametrize("name", FB_CASES[:8] + ["G9_caustic_lt_64x64_spp16", "G12_hardlight_pt_64x64_spp16"])
+def test_gpu_both_sweep_builds_match_reference_golden(name, build, max_rr, golden_manifest, monkeypatch):
+    monkeypatch.setenv("BDPT_SPLIT_MAX_RR", max_rr)
+    m = golden_manifest["framebuffers"][name]
+    it = integrator(m["scene"], m["width"], m["height"], m["spp"], m["rr_depth"], STRATEGY[m.get("strategy", "bdpt")])
+    fb = it.render_frame(row_offset=0, row_stride=m["row_stride"]).reshape(-1)
+    assert it.stats()["kernel"] == ("bdpt_frame_kernel_split" if build == "split" else "bdpt_frame_kernel")
+    worst, exact, whole = report(fb, load_golden(name))
+    assert worst <= TOL, f"{build}: max per-pixel rel L2 {worst:.3g} (bit-exact floats {exact:.4f})"

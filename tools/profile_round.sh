@@ -15,9 +15,20 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 B="python3 $R/bench.py --no-cpu --scene $SCENE --width $W --height $H --spp $SPP"
-K="bdpt_frame_kernel<false, false, false>"
+K=${KERNEL:-"bdpt_frame_kernel<false, false, false>"}  # KERNEL=bdpt_frame_kernel_split<...> for rrDepth <= 3 scenes
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_$WL -o kt --output-format csv -- $B --steps 2 --warmup 1 > $OUT/kt_$WL.log 2>&1
+# the frame-kernel build that ran (bdpt_frame_kernel, _split for rrDepth <= 3, ...), unless KERNEL names it
+if [ -z "$KERNEL" ]; then
+  K=$(python3 - "$(find $OUT/kt_$WL -name '*kernel_stats.csv' | head -1)" <<'PY'
+import csv, re, sys
+best = max((r for r in csv.DictReader(open(sys.argv[1])) if "bdpt_frame_kernel" in r["Name"]),
+           key=lambda r: float(r["TotalDurationNs"]))
+print(re.search(r"(bdpt_frame_kernel\w*<[^>]*>)", best["Name"]).group(1))
+PY
+)
+fi
+echo "frame kernel: $K"
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch_$WL -o fetch --output-format csv -- $B --steps 1 --warmup 0 > $OUT/fetch_$WL.log 2>&1
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/write_$WL -o write --output-format csv -- $B --steps 1 --warmup 0 > $OUT/write_$WL.log 2>&1
 i=0
