@@ -462,6 +462,7 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     c->sc.mt_ring = nullptr;
     c->sc.mt_ring_stride = 0;
     c->sc.nemit = static_cast<int32_t>(L.emitters.size());
+    c->sc.inv_nemit = 1.f / static_cast<float>(c->sc.nemit);  // the device's 1.f / nemit, bit for bit
     c->sc.nbsdf = static_cast<int32_t>(L.bsdfs.size());
     c->sc.nshapes = static_cast<int32_t>(L.shape_emitter.size());
     {  // LDS table layout (bdpt_device.hpp scene_tables_to_lds), 16-byte aligned parts
@@ -552,6 +553,8 @@ static dev::DevFrame make_frame(const bdpt_frame_params* p) {
     fr.rr_mode = p->russian_roulette == BDPT_RR_LUMINANCE ? 1 : 0;
     fr.depth_cap = fr.rr_mode ? kRrDepthGuard : p->rr_depth;
     fr.lv_max = fr.rr_mode ? std::max(kRrLightVerts, p->rr_depth - 1) : std::max(p->rr_depth - 1, 1);
+    fr.inv_spp = 1.f / static_cast<float>(fr.spp);  // IEEE divisions: the bits of the device's rcp_cr
+    fr.inv_pixels = 1.f / static_cast<float>(fr.W * fr.H);
     fr.capped = nullptr;  // the context's word, set by the caller
     return fr;
 }

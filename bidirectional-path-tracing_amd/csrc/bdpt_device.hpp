@@ -56,6 +56,7 @@ struct DevScene {
     // bdpt_capi.cpp): the padded boxes make a plain tn <= tf conservative
     uint32_t node_slack;
     int32_t nemit, nbsdf, nshapes;
+    float inv_nemit;  // 1 / nemit (the host's IEEE division): selectEmitter's pdf (core.h emitter selection)
     // LDS copy of the small tables (scene_tables_to_lds): word offsets of the
     // emitter records and the shape->emitter map, total words (16-byte rounded)
     uint32_t lds_emit_off, lds_shape_off, lds_words;
@@ -156,6 +157,10 @@ struct DevFrame {
     int32_t depth_cap;  // subpath depth bound: rr_depth under NO_RR; with RR a guard (2^20 bounces)
     int32_t lv_max;     // light vertices a lane slot stores: rr_depth - 1 under NO_RR, more with RR
     uint32_t* capped;   // RR: samples that hit depth_cap or lv_max (the frame is then not the reference's)
+    // 1 / spp and 1 / (W * H) as the host's IEEE divisions, the bits the device's correctly
+    // rounded reciprocal (rcp_cr) and division give: per-frame constants the shading bodies
+    // would otherwise recompute (~10 instructions each) per splat and per sample
+    float inv_spp, inv_pixels;
 };
 
 struct Ray {
@@ -1447,7 +1452,7 @@ __device__ __forceinline__ int sample_emitter(const DevScene& sc, Rng& rng, floa
     const float u0 = next1(rng);
     uint32_t id = static_cast<uint32_t>(u0 * static_cast<float>(sc.nemit));
     id = id < static_cast<uint32_t>(sc.nemit - 1) ? id : static_cast<uint32_t>(sc.nemit - 1);
-    emitter_pdf = 1.f / static_cast<float>(sc.nemit);
+    emitter_pdf = sc.inv_nemit;  // 1.f / nemit
     const EmitterRecord& e = emitter_of(sc, static_cast<int>(id));
     const bool lds = sc.lds_etri_off != kNoLds;  // uniform: LDS copies of the faces and CDFs
     const float* cdf = lds ? reinterpret_cast<const float*>(g_scene_lds + sc.lds_ecdf_off) : sc.emit_cdf;

@@ -305,7 +305,7 @@ __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __res
     if (COUNT) cnt.c[7] += L.rng.n;
     // rgb[p] += acc * (1 / spp) (renderer.cpp:202), one sample at a time.
     if (!(fr.flags & kFlagNoEyeAccum) && (L.c.Li.x != 0.f || L.c.Li.y != 0.f || L.c.Li.z != 0.f)) {
-        const float inv_spp = 1.f / static_cast<float>(fr.spp);
+        const float inv_spp = fr.inv_spp;  // 1.f / spp
         const f3 add = L.c.Li * inv_spp;
 #if BDPT_EYE_SLOTS && !BDPT_SAMPLER_STATE
         float4* const s = wave_eye_slots();
@@ -420,8 +420,8 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
         const float nlight = static_cast<float>(fr.W * fr.H); \
         f3 rad = L.c.tp * (f * rcp_cr(wi.z)); \
         rad = rad * rcp_cr(surf2img); \
-        rad = rad * rcp_cr(nlight); \
-        rad = rad * rcp_cr(static_cast<float>(fr.spp)); \
+        rad = rad * fr.inv_pixels;  /* rcp(nlight) */ \
+        rad = rad * fr.inv_spp;  /* rcp(spp) */ \
         const float reversePdf_a = 1.f * img2surf; \
         const float prevRev = ep.rev * (rr_on(fr) ? L.c.rr : 1.f);  /* swapped (wi, wo) * lightVertex.rr (bdpt.h:342) */ \
         const float lightWeight = div_cr(reversePdf_a, nlight) * (L.c.vcm + prevRev * L.c.vc); \
@@ -527,7 +527,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             const int eid = shape_emitter_of(sc, L.h.shape);
             if (eid >= 0) {  // (the reference asserts otherwise, integrator.cpp:56)
                 const EmitterRecord& e = emitter_of(sc, eid);
-                const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
+                const float emitterPdf = sc.inv_nemit;  // 1.f / nemit
                 if (L.c.depth > 1) {
                     f3 contrib = ld3(e.radiance) * L.c.tp;
                     const float pA = rcp_cr(e.area * emitterPdf);
