@@ -2,10 +2,12 @@
 #include "wide_bvh.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <string>
 
 #include "scene.hpp"
 
@@ -158,11 +160,77 @@ float u2f(uint32_t u) {
 
 // Collapses the binary tree to 4-wide nodes (repeatedly opening the interior
 // child of largest area) into out.nodes; returns the root link.
+// The children of every 4-wide node are chosen by dynamic programming over the
+// binary tree to minimise the SAH cost (area-weighted node and triangle tests,
+// BDPT_DP_NODE_COST per node test, 1 per triangle; round 3: HardLight +1.6 %,
+// Caustic / synth1m +-0.2 %, 13 % fewer nodes). BDPT_WIDE_COLLAPSE=greedy
+// restores the earlier rule: open the largest interior child first.
+struct DpCollapse {
+    std::vector<std::array<double, kWideArity + 1>> dist;  // [j]: best cost of the subtree as <= j children
+    std::vector<std::array<int, kWideArity + 1>> cut;      // [j]: 0 = the subtree itself, else slots to the left
+    std::vector<double> cost;                              // the subtree as one child (a leaf, or a wide node)
+    std::vector<int> wide_cut;                             // a wide node here: slots given to the left child
+    void run(const std::vector<BNode>& bn, double node_cost) {
+        const size_t n = bn.size();
+        dist.assign(n, {});
+        cut.assign(n, {});
+        cost.assign(n, 0.0);
+        wide_cut.assign(n, 1);
+        std::function<void(int)> visit = [&](int id) {
+            const BNode& b = bn[id];
+            const double area = b.box.area();
+            if (b.leaf >= 0) {
+                cost[id] = area * b.count;
+                for (int j = 1; j <= kWideArity; j++) dist[id][j] = cost[id], cut[id][j] = 0;
+                return;
+            }
+            visit(b.left);
+            visit(b.right);
+            double best = __builtin_inf();
+            for (int i = 1; i < kWideArity; i++) {
+                const double c = dist[b.left][i] + dist[b.right][kWideArity - i];
+                if (c < best) best = c, wide_cut[id] = i;
+            }
+            cost[id] = area * node_cost + best;
+            dist[id][1] = cost[id], cut[id][1] = 0;
+            for (int j = 2; j <= kWideArity; j++) {
+                dist[id][j] = cost[id], cut[id][j] = 0;
+                for (int i = 1; i < j; i++) {
+                    const double c = dist[b.left][i] + dist[b.right][j - i];
+                    if (c < dist[id][j]) dist[id][j] = c, cut[id][j] = i;
+                }
+            }
+        };
+        visit(0);
+    }
+    void gather(const std::vector<BNode>& bn, int id, int j, std::vector<int>& out) const {
+        if (cut[id][j] == 0) {
+            out.push_back(id);
+            return;
+        }
+        gather(bn, bn[id].left, cut[id][j], out);
+        gather(bn, bn[id].right, j - cut[id][j], out);
+    }
+};
+
 uint32_t collapse(const std::vector<BNode>& bn, const std::function<uint32_t(const BNode&)>& leaf_link, WideBvh& out) {
     int max_stack = 0, max_depth = 0;
+    const char* mode = std::getenv("BDPT_WIDE_COLLAPSE");
+    const bool dp = !(mode && std::string(mode) == "greedy");
+    DpCollapse D;
+    if (dp) {
+        const char* nc = std::getenv("BDPT_DP_NODE_COST");
+        D.run(bn, nc ? std::max(0.0, std::atof(nc)) : 1.0);
+    }
     std::function<uint32_t(int, int, int)> emit = [&](int id, int depth, int stack_above) -> uint32_t {
-        std::vector<int> ch = {bn[id].left, bn[id].right};
-        while (static_cast<int>(ch.size()) < kWideArity) {
+        std::vector<int> ch;
+        if (dp) {
+            D.gather(bn, bn[id].left, D.wide_cut[id], ch);
+            D.gather(bn, bn[id].right, kWideArity - D.wide_cut[id], ch);
+        } else {
+            ch = {bn[id].left, bn[id].right};
+        }
+        while (!dp && static_cast<int>(ch.size()) < kWideArity) {
             int pick = -1;
             double area = -1.0;
             for (int k = 0; k < static_cast<int>(ch.size()); k++)

@@ -12,7 +12,8 @@
 //
 // That frees the hierarchy ABOVE the leaves: this builder groups the
 // reference leaves (kept as units: same triangles, same order, same exact box)
-// under a binned-SAH tree collapsed to 4-wide nodes. Interior boxes are exact
+// under a binned-SAH tree collapsed to 4-wide nodes (children picked by SAH
+// dynamic programming, wide_bvh.cpp DpCollapse). Interior boxes are exact
 // unions of leaf boxes and are tested conservatively (an ambiguous fast test
 // counts as a hit); the leaf boxes are tested exactly. Rays with a zero or
 // non-finite reciprocal direction (where 0/0 = NaN breaks monotonicity) keep
