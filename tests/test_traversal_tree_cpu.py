@@ -124,3 +124,18 @@ def test_single_triangle_scene_is_one_leaf(tmp_path):
     _, _, _, root = s.export_traversal()
     assert root == (LEAF_BIT | (0 << 3) | 1)
     check_tree(s, tri_tree=True)
+
+
+@pytest.mark.parametrize("scene_name", SCENES)
+def test_greedy_collapse_tree_preconditions_and_dp_is_smaller(scene_name, monkeypatch):
+    """The 4-wide grouping by SAH dynamic programming (the default, wide_bvh.cpp
+    DpCollapse) and the earlier largest-child-first rule (BDPT_WIDE_COLLAPSE=greedy)
+    group the same binary tree: same traversal leaves, both meet the preconditions,
+    and the DP tree needs no more nodes (it fills the 4 slots where the SAH says so)."""
+    dp = bdpt_amd.Scene(variants.obj_path(scene_name))
+    monkeypatch.setenv("BDPT_WIDE_COLLAPSE", "greedy")
+    greedy = bdpt_amd.Scene(variants.obj_path(scene_name))
+    check_tree(greedy, tri_tree=True)
+    a, b = dp.info(), greedy.info()
+    assert a["wide_leaves"] == b["wide_leaves"]
+    assert a["wide_nodes"] <= b["wide_nodes"]
