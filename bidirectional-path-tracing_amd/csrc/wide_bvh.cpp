@@ -42,7 +42,8 @@ struct BNode {  // binary build node
     int count = 1;
 };
 
-constexpr int kBins = 32;
+constexpr int kMaxBins = 128;
+constexpr int kBins = 32;  // SAH bins per axis (BDPT_SAH_BINS overrides, up to kMaxBins)
 constexpr int kMaxBinaryDepth = 96;
 
 class Builder {
@@ -55,6 +56,7 @@ class Builder {
     // node_cost * area + the best split); max_leaf 1 = one item per leaf.
     int max_leaf = 1;
     double node_cost = 1.0;
+    int bins = kBins;
 
     int build(int b, int e, int depth) {
         max_depth = std::max(max_depth, depth);
@@ -106,22 +108,22 @@ class Builder {
         int best_axis = -1, best_bin = -1;
         for (int a = 0; a < 3; a++) {
             if (!(ch[a] > cl[a])) continue;
-            const double scale = kBins / (double(ch[a]) - cl[a]);
-            Box bb[kBins];
-            int cnt[kBins] = {};
-            for (int k = 0; k < kBins; k++) bb[k].clear();
+            const double scale = bins / (double(ch[a]) - cl[a]);
+            Box bb[kMaxBins];
+            int cnt[kMaxBins] = {};
+            for (int k = 0; k < bins; k++) bb[k].clear();
             for (int i = b; i < e; i++) {
                 int k = static_cast<int>((double(L[i].c[a]) - cl[a]) * scale);
-                k = std::min(std::max(k, 0), kBins - 1);
+                k = std::min(std::max(k, 0), bins - 1);
                 cnt[k]++;
                 bb[k].grow(L[i].box);
             }
-            double right_area[kBins];
-            int right_cnt[kBins];
+            double right_area[kMaxBins];
+            int right_cnt[kMaxBins];
             Box acc;
             acc.clear();
             int n = 0;
-            for (int k = kBins - 1; k > 0; k--) {
+            for (int k = bins - 1; k > 0; k--) {
                 acc.grow(bb[k]);
                 n += cnt[k];
                 right_area[k] = acc.area();
@@ -129,7 +131,7 @@ class Builder {
             }
             acc.clear();
             n = 0;
-            for (int k = 0; k < kBins - 1; k++) {
+            for (int k = 0; k < bins - 1; k++) {
                 acc.grow(bb[k]);
                 n += cnt[k];
                 if (n == 0 || right_cnt[k + 1] == 0) continue;
@@ -139,11 +141,11 @@ class Builder {
         }
         if (best_axis < 0) return median(b, e, wide_axis);
         if (cost_out) *cost_out = best;
-        const double scale = kBins / (double(ch[best_axis]) - cl[best_axis]);
+        const double scale = bins / (double(ch[best_axis]) - cl[best_axis]);
         const float lo = cl[best_axis];
         auto it = std::partition(L.begin() + b, L.begin() + e, [&](const Leaf& x) {
             int k = static_cast<int>((double(x.c[best_axis]) - lo) * scale);
-            k = std::min(std::max(k, 0), kBins - 1);
+            k = std::min(std::max(k, 0), bins - 1);
             return k <= best_bin;
         });
         const int mid = static_cast<int>(it - L.begin());
@@ -298,6 +300,7 @@ bool build_wide_bvh(const std::vector<FlatNode>& flat, WideBvh& out, std::string
         return true;
     }
     Builder B(leaves);
+    if (const char* e = std::getenv("BDPT_SAH_BINS")) B.bins = std::min(kMaxBins, std::max(2, std::atoi(e)));
     B.build(0, static_cast<int>(leaves.size()), 0);
     if (B.max_depth > kMaxBinaryDepth) {  // degenerate SAH splits: fall back to a balanced tree
         Builder M(leaves);
@@ -372,6 +375,7 @@ bool build_wide_bvh_tris(const std::vector<FlatNode>& flat, const std::vector<fl
     Builder B(items);
     B.max_leaf = leaf_max;
     B.node_cost = node_cost;
+    if (const char* e = std::getenv("BDPT_SAH_BINS")) B.bins = std::min(kMaxBins, std::max(2, std::atoi(e)));
     B.build(0, static_cast<int>(n), 0);
     if (B.max_depth > kMaxBinaryDepth) {
         Builder M(items);
