@@ -76,6 +76,7 @@ def algorithmic_write_bytes(c: dict, samples: int) -> float:
 # Reference CPU cost per camera sample and thread (measured on the GPU box's host,
 # round 1) — only sizes the bounded CPU sample.
 CPU_US_PER_SAMPLE = {"caustic": 18.0, "hardlight": 5.0, "hardlight_mirror": 9.0, "cbox_low": 9.0, "synth1m": 35.0}
+RR_CPU_FACTOR = 3.5  # Russian roulette: subpaths continue past rrDepth (Caustic 512², 8 threads: 3.5x)
 
 
 def host_cpus() -> dict:
@@ -103,16 +104,18 @@ def host_cpus() -> dict:
 
 
 def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int, integrator: str = "bdpt",
-                 frame_out: str | None = None) -> dict:
+                 frame_out: str | None = None, russian_roulette: bool = False) -> dict:
     """The reference CPU path (oracle/_ref/ref_bdpt = the unmodified reference
     BDPT compiled from its sources) on a bounded sample of the same workload:
     every `stride`-th row of the image at the bench spp, std::thread over every
     host core this job may use. With `frame_out`, the reference's framebuffer of
     that row shard is written there (for the in-run parity check). Falls back to
-    the C restatement (kind "port") when the reference binary is absent."""
+    the C restatement (kind "port") when the reference binary is absent. With
+    russian_roulette the reference is the NO_RR = 0 build (oracle/_ref/ref_bdpt_rr,
+    bdpt.h:18 flipped)."""
     cpus = host_cpus()
     threads = cpus["usable"]
-    ref = os.path.join(REPO, "oracle", "_ref", "ref_bdpt")
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_bdpt_rr" if russian_roulette else "ref_bdpt")
     toml = os.path.join("/tmp", f"bench_{scene}_{os.getpid()}.toml")
     with open(toml, "w") as f:
         if integrator == "bdpt":
@@ -122,7 +125,8 @@ def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int, integrator: str 
         else:
             f.write(variants.direct_toml_text(scene, W, H, spp))
     # about 15 s of wall time at the reference's per-sample cost on one thread
-    target_samples = 15.0 * threads / (CPU_US_PER_SAMPLE.get(scene, 20.0) * 1e-6)
+    us = CPU_US_PER_SAMPLE.get(scene, 20.0) * (RR_CPU_FACTOR if russian_roulette else 1.0)
+    target_samples = 15.0 * threads / (us * 1e-6)
     stride = max(1, int(round(H * W * spp / max(target_samples, 1.0))))
     stride = min(stride, H)
     if os.path.exists(ref):
@@ -138,7 +142,7 @@ def cpu_baseline(scene: str, W: int, H: int, spp: int, rr: int, integrator: str 
         import oracle as O
         sc = O.Scene(variants.obj_path(scene))
         cam = variants.SCENES[scene]["camera"]
-        p = (O.make_params(cam, W, H, spp, rr) if integrator == "bdpt" else
+        p = (O.make_params(cam, W, H, spp, rr, russian_roulette=int(russian_roulette)) if integrator == "bdpt" else
              O.make_path_params(cam, W, H, spp) if integrator == "path" else O.make_direct_params(cam, W, H, spp))
         t = time.time()
         fbo, samples = sc.render(p, threads=threads, rows=list(range(0, H, stride)))
@@ -174,6 +178,38 @@ def stamped(path: str, build: str) -> dict | None:
     return d if d.get("kernel_build") == build else None
 
 
+def pm_scale(pm: dict, samples: int) -> float:
+    """Launch-size ratio of a profiled launch to this run's (the stamped files are
+    per launch of the same workload; 1.0 when the sample counts agree)."""
+    return pm["samples_per_launch"] / max(samples, 1)
+
+
+def issue_roofline(deep: dict, kernel_s: float) -> dict | None:
+    """The issue roofline the frame kernel is under, from the
+    build-stamped pmc_deep counters of one launch and that launch's duration:
+      clock           = GRBM_GUI_ACTIVE / XCDs / kernel_s (effective shader clock)
+      valu_issue_frac = SQ_INSTS_VALU / (CUs * 4 SIMDs * clock / 2 * kernel_s)
+                        (a wave64 VALU instruction issues over 2 cycles)
+      lane_frac       = valu_issue_frac * active_lane_frac (of the FP32 vector lane peak)
+    plus VALU / SALU wave instructions per sample."""
+    c = deep.get("counters_per_launch") or {}
+    gui, valu = c.get("GRBM_GUI_ACTIVE"), c.get("SQ_INSTS_VALU")
+    if not gui or not valu or kernel_s <= 0:
+        return None
+    xcds, cus = 8, deep.get("cus", 256)
+    clock = gui / xcds / kernel_s
+    issue_frac = valu / (cus * 4 * clock / 2 * kernel_s)
+    lanes = deep.get("active_lane_frac")
+    out = {"bound": "VALU issue", "clock_ghz": round(clock * 1e-9, 3), "valu_issue_frac": round(issue_frac, 4),
+           "active_lane_frac": lanes, "lane_frac": round(issue_frac * lanes, 4) if lanes else None,
+           "valu_insts_per_sample": deep.get("valu_insts_per_sample"),
+           "salu_insts_per_sample": deep.get("salu_insts_per_sample"),
+           "wait_frac": deep.get("wait_frac"), "source": deep.get("source"),
+           "formula": "lane_frac = SQ_INSTS_VALU / (CUs * 4 * clock / 2 * s) * active_lane_frac, "
+                      "clock = GRBM_GUI_ACTIVE / 8 / s"}
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -185,6 +221,10 @@ def main() -> None:
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--rr-depth", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--russian-roulette", action="store_true",
+                    help="the reference's NO_RR = 0 branch (bdpt.h:18, :68, :129-132, :188, :201-204): subpaths "
+                         "continue past rrDepth by roulette; the bdpt_frame_kernel_rr build, checked against "
+                         "oracle/_ref/ref_bdpt_rr")
     ap.add_argument("--integrator", choices=["bdpt", "path", "direct"], default="bdpt",
                     help="bdpt = the hot path (BASELINE metric); path = the reference's PathTracerIntegrator "
                          "(path.h, cbox_bdpt_path.toml settings), direct = its DirectIntegrator (direct.h, MIS, "
@@ -217,7 +257,11 @@ def main() -> None:
     sc = variants.SCENES[args.scene]
     rr = args.rr_depth or sc["rr_depth"]
     W, H, spp = args.width, args.height, args.spp
-    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**sc["camera"]), width=W, height=H, spp=spp, rr_depth=rr)
+    rrm = bdpt_amd.RR_LUMINANCE if args.russian_roulette else bdpt_amd.RR_NONE
+    if args.russian_roulette and args.integrator != "bdpt":
+        sys.exit("--russian-roulette is the BDPT integrator's NO_RR switch")
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**sc["camera"]), width=W, height=H, spp=spp, rr_depth=rr,
+                          russian_roulette=rrm)
     if args.integrator == "path":
         integ = bdpt_amd.PathTracerIntegrator(bdpt_amd.Scene(variants.obj_path(args.scene)), cfg,
                                               bdpt_amd.PathSettings(), device=gpu if world > 1 else 0)
@@ -231,7 +275,7 @@ def main() -> None:
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    kernel_ms, reduce_ms = [], []
+    kernel_ms, reduce_ms, tail_ms, capped = [], [], [], []
 
     row_offset, row_stride = bdpt_dist.row_shard(rank, world)
 
@@ -240,6 +284,8 @@ def main() -> None:
         integ.render_device(fb.data_ptr(), stream, row_offset=row_offset, row_stride=row_stride)
         st = integ.stats()  # waits for the render kernel's end event
         kernel_ms.append(st["kernel_ms"])
+        tail_ms.append(st.get("tail_ms", 0.0))
+        capped.append(st.get("capped_samples", 0))
         if args.integrator == "path":
             integ.check_levels()  # a sample past the 512-level stack would not be the reference's
         if world > 1:  # the exchange step, timed on its own (host wall: it includes waiting for slower ranks)
@@ -252,6 +298,8 @@ def main() -> None:
         step()
     kernel_ms.clear()
     reduce_ms.clear()
+    tail_ms.clear()
+    capped.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -303,7 +351,8 @@ def main() -> None:
         print(json.dumps(out), flush=True)
     elif rank == 0:
         # algorithmic bytes per sample from a counting pass (untimed, same seeds, smaller spp)
-        cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=min(spp, 16), rr_depth=rr)
+        cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=min(spp, 16), rr_depth=rr,
+                                  russian_roulette=rrm)
         cnt = bdpt_amd.BDPTIntegrator(integ.scene, cnt_cfg, device=gpu if world > 1 else 0)
         cbuf = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
         cnt.render_device(cbuf.data_ptr(), stream, flags=bdpt_amd.FLAG_COUNT)
@@ -313,7 +362,7 @@ def main() -> None:
         bps_layout = algorithmic_bytes_per_sample(cts, cst["samples"], LAYOUT_BYTES)
         kernel_s = avg_kernel_ms * 1e-3
         achieved = bps * local_samples / kernel_s / 1e9
-        workload = f"{args.scene}_{W}x{H}_{spp}spp"
+        workload = f"{args.scene}_{W}x{H}_{spp}spp" + ("_rr" if args.russian_roulette else "")
         build = bdpt_amd.kernel_build_hash()
         # measured memory-side traffic and issue counters of THIS kernel build
         # (rocprofv3 --pmc passes, tools/profile_round.sh / tools/pmc_deep.sh)
@@ -330,7 +379,10 @@ def main() -> None:
                 "bytes_per_sample": round(bps, 1),
                 "bytes_per_sample_layout_model": round(bps_layout, 1),
                 "achieved_layout_model": round(bps_layout * local_samples / kernel_s / 1e9, 2),
-                "counts_per_sample": {k: round(v / cst["samples"], 3) for k, v in cts.items()}}
+                "counts_per_sample": {k: round(v / cst["samples"], 3) for k, v in cts.items()},
+                # the persistent grid's end tail (device clock: the frame's last 64-sample chunk
+                # claimed -> last wave done), what a 1/N row shard pays again per rank
+                "tail_ms": round(sum(tail_ms) / max(len(tail_ms), 1), 3)}
         if traffic is not None:
             roof["dram_achieved"] = round(traffic / kernel_s / 1e9, 2)
             roof["dram_frac"] = round(traffic / kernel_s / 1e9 / HBM_PEAK_GBPS, 5)
@@ -351,7 +403,11 @@ def main() -> None:
             for k in ("active_lane_frac", "valu_issue_frac", "wait_frac", "valu_insts_per_sample"):
                 roof[k] = deep.get(k)
             roof["issue_source"] = deep.get("source")
-        default_workload = (args.scene, W, H, spp) == ("caustic", 512, 512, 256)
+            issue = issue_roofline(deep, kernel_s * pm_scale(deep, local_samples))
+            if issue:
+                roof["issue"] = issue
+                roof["binding"] = issue["bound"]
+        default_workload = (args.scene, W, H, spp) == ("caustic", 512, 512, 256) and not args.russian_roulette
         out = {
             "metric": METRIC if default_workload else f"Msamples/sec (whole node), {SCENE_LABEL.get(args.scene, args.scene)} "
                                                       f"{W}x{H} at {spp} spp",
@@ -367,17 +423,26 @@ def main() -> None:
             "dtype": "f32",
             "data": ("synthetic camera samples over the reference's own scene files" if args.scene != "synth1m"
                      else "synthetic camera samples over a generated 1M-triangle scene"),
-            "config": {"workload": f"{args.scene}_{W}x{H}_{spp}spp", "scene": SCENE_LABEL.get(args.scene, args.scene),
+            "config": {"workload": workload, "scene": SCENE_LABEL.get(args.scene, args.scene),
                        "width": W, "height": H, "spp": spp, "rr_depth": rr, "samples_per_step": samples_total,
                        "parallelism": (f"{world}-way row-interleaved shards + one framebuffer sum-reduce "
                                        f"({ranks['backend']})" if ranks else "one GPU, whole image (no reduce)")},
             "roofline": roof,
         }
+        if args.russian_roulette:
+            # Russian roulette: subpath depth is unbounded (bdpt.h:68, :188); the timed frames'
+            # samples that met the store / bounce bounds (must be 0) and the counting pass's maxima
+            out["config"]["russian_roulette"] = "NO_RR = 0 (bdpt.h:18)"
+            out["russian_roulette"] = {"capped_samples_per_step": capped, "counting_pass_spp": cnt_cfg.spp,
+                                       "max_light_depth": cst.get("max_light_depth"),
+                                       "max_eye_depth": cst.get("max_eye_depth"),
+                                       "max_queries_per_sample": cst.get("max_queries"),
+                                       "tail_ms": roof["tail_ms"], "kernel": cst.get("kernel")}
         if ranks:
             out["ranks"] = ranks
         if world == 1 and not args.no_cpu:
             ref_fb = None if args.no_parity else os.path.join("/tmp", f"bench_ref_fb_{os.getpid()}.f32")
-            cb = cpu_baseline(args.scene, W, H, spp, rr, frame_out=ref_fb)
+            cb = cpu_baseline(args.scene, W, H, spp, rr, frame_out=ref_fb, russian_roulette=args.russian_roulette)
             out["cpu_baseline"] = {k: v for k, v in cb.items() if k != "row_stride"}
             if ref_fb is not None:
                 import numpy as np

@@ -109,7 +109,8 @@ MAX_DEVICES = 16  # BDPT_MAX_DEVICES
 class _MultiStats(ctypes.Structure):  # bdpt_multi_stats
     _fields_ = [("devices", ctypes.c_int32), ("rccl", ctypes.c_int32), ("wall_ms", ctypes.c_double),
                 ("render_ms", ctypes.c_double), ("reduce_ms", ctypes.c_double), ("samples", ctypes.c_int64),
-                ("kernel_ms", ctypes.c_double * MAX_DEVICES), ("device_samples", ctypes.c_int64 * MAX_DEVICES)]
+                ("kernel_ms", ctypes.c_double * MAX_DEVICES), ("device_samples", ctypes.c_int64 * MAX_DEVICES),
+                ("capped_samples", ctypes.c_int64)]
 
 
 class _MaterialDesc(ctypes.Structure):  # bdpt_material_desc
@@ -139,7 +140,7 @@ class _SceneDesc(ctypes.Structure):  # bdpt_scene_desc
 # BsdfKind (bdpt_types.h) -> the MTL illum that selects it (renderer.cpp:258-271)
 KIND_ILLUM = {0: 5, 1: 7, 2: 3, 3: 6, 4: 8, 5: 2}
 LAYOUT_ARRAYS = ("tri", "shade", "nodes", "wnodes", "wtri", "lbox", "bsdfs", "emitters", "emit_tri", "emit_cdf",
-                 "shape_emitter", "roots")  # bdpt_scene_export_layout ids 0..11
+                 "shape_emitter", "roots", "bsdfs_ingested")  # bdpt_scene_export_layout ids 0..12
 
 
 @dataclass
@@ -167,7 +168,9 @@ BVH_NODE_DTYPE = np.dtype([("bmin", "<f4", 3), ("bmax", "<f4", 3), ("start", "<u
 class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("samples", ctypes.c_int64), ("launches", ctypes.c_int64),
                 ("counters", ctypes.c_int64 * len(COUNTER_NAMES)),  # BDPT_NUM_COUNTERS
-                ("capped_samples", ctypes.c_int64)]
+                ("capped_samples", ctypes.c_int64), ("span_ms", ctypes.c_double), ("tail_ms", ctypes.c_double),
+                ("max_light_depth", ctypes.c_int64), ("max_eye_depth", ctypes.c_int64),
+                ("max_queries", ctypes.c_int64)]
 
 
 # Sources that make up the frame kernels' code objects: their hash stamps the
@@ -213,7 +216,7 @@ def lib():
         L.bdpt_scene_get_info.argtypes = [vp, ctypes.POINTER(_SceneInfo)]
         L.bdpt_scene_export.argtypes = [vp, vp, vp, vp, vp]
         L.bdpt_scene_export_traversal.argtypes = [vp, vp, vp, vp, vp]
-        L.bdpt_intersect_from.argtypes = [vp, ctypes.c_int64, vp, vp, i32, vp]
+        L.bdpt_intersect_from.argtypes = [vp, ctypes.c_int64, vp, vp, vp, i32, vp]
         L.bdpt_scene_create.argtypes = [ctypes.POINTER(_SceneDesc), ctypes.POINTER(vp)]
         L.bdpt_scene_export_layout.argtypes = [vp, i32, vp, ctypes.POINTER(ctypes.c_int64)]
         L.bdpt_camera_constants.argtypes = [ctypes.POINTER(_Camera), i32, i32, f32p]
@@ -515,13 +518,13 @@ class Scene:
 
     def to_desc(self) -> SceneDesc:
         """The descriptor of this scene, rebuilt from its exports (BVH leaf order back
-        to (shape, face) order; materials and emitters from the device records)."""
+        to (shape, face) order; materials and emitters from the ingested records)."""
         inf = self.info()
         tf, ti, nf, nu = self.export()
         perm = np.lexsort((ti[:, 1], ti[:, 0]))  # (shape, prim) order
         order = np.empty_like(perm)
         order[perm] = np.arange(perm.size)
-        rec = np.frombuffer(self.export_layout("bsdfs"), np.uint32).reshape(-1, 18)
+        rec = np.frombuffer(self.export_layout("bsdfs_ingested"), np.uint32).reshape(-1, 18)
         recf = rec.view(np.float32)
         mats = [dict(illum=KIND_ILLUM[int(r[0])], kd=f[2:5], ks=f[5:8], tf=f[8:11], ke=f[11:14], ns=f[14], ni=f[15],
                      scale=f[16], spec_weight=f[17]) for r, f in zip(rec, recf)]
@@ -670,18 +673,23 @@ class BDPTIntegrator:
                                       wi.ctypes.data, pdf.ctypes.data))
         return f, wi, pdf
 
-    def intersect(self, rays, occlusion: bool = False, origin_normals=None) -> np.ndarray:
+    def intersect(self, rays, occlusion: bool = False, origin_normals=None, origin_tris=None) -> np.ndarray:
         """AcceleratorBVH::intersect (accel.h:125-172) or the occlusion query of
         visibilityQuery (bvh.h:259-352) on rays (n, 8): a structured bdpt_hit array.
-        origin_normals (n, 3): the surfaces the rays leave, for the frames' near-cull
-        rule (bdpt_intersect_from); None: no near cull."""
+        origin_normals (n, 3): the surfaces the rays leave (the path's interpolated
+        shading normals), origin_tris (n,): their triangles (bdpt_hit.tri order, -1:
+        none), for the frames' near-cull rule (bdpt_intersect_from); None: no near cull."""
         r = _af32(rays, 8)
         out = np.zeros(r.shape[0], HIT_DTYPE)
         if origin_normals is None:
             _check(lib().bdpt_intersect(self._h, r.shape[0], r.ctypes.data, 1 if occlusion else 0, out.ctypes.data))
         else:
             nr = _af32(origin_normals, 3)
-            _check(lib().bdpt_intersect_from(self._h, r.shape[0], r.ctypes.data, nr.ctypes.data, 1 if occlusion else 0,
+            ot = None if origin_tris is None else np.ascontiguousarray(origin_tris, np.int32).reshape(-1)
+            if ot is not None and ot.shape[0] != r.shape[0]:
+                raise ValueError("origin_tris needs one entry per ray")
+            _check(lib().bdpt_intersect_from(self._h, r.shape[0], r.ctypes.data, nr.ctypes.data,
+                                             None if ot is None else ot.ctypes.data, 1 if occlusion else 0,
                                              out.ctypes.data))
         return out
 
@@ -712,6 +720,8 @@ class BDPTIntegrator:
         _check(lib().bdpt_get_stats(self._h, ctypes.byref(s)))
         return dict(kernel_ms=s.kernel_ms, samples=s.samples, launches=s.launches,
                     counters=dict(zip(COUNTER_NAMES, list(s.counters))), capped_samples=s.capped_samples,
+                    span_ms=s.span_ms, tail_ms=s.tail_ms, max_light_depth=s.max_light_depth,
+                    max_eye_depth=s.max_eye_depth, max_queries=s.max_queries,
                     kernel=(lib().bdpt_last_kernel(self._h) or b"").decode())
 
     def synchronize(self) -> None:
@@ -843,7 +853,8 @@ class MultiDeviceRenderer:
         _check(lib().bdpt_multi_get_stats(self._h, ctypes.byref(s)))
         n = s.devices
         return dict(devices=n, rccl=bool(s.rccl), wall_ms=s.wall_ms, render_ms=s.render_ms, reduce_ms=s.reduce_ms,
-                    samples=s.samples, kernel_ms=list(s.kernel_ms)[:n], device_samples=list(s.device_samples)[:n])
+                    samples=s.samples, kernel_ms=list(s.kernel_ms)[:n], device_samples=list(s.device_samples)[:n],
+                    capped_samples=s.capped_samples)
 
 
 def debug_math(fn: str, x: np.ndarray, y: np.ndarray | None = None, device: int = 0) -> np.ndarray:

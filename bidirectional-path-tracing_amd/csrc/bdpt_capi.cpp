@@ -36,7 +36,7 @@ hipError_t launch_bsdf_kat(const dev::DevScene& sc, int mode, int64_t n, const i
 hipError_t launch_fresnel_kat(int64_t n, const float* in, float* out, hipStream_t st);
 hipError_t launch_triangle_kat(int64_t n, const float* rays, const float* verts, float* out, hipStream_t st);
 hipError_t launch_intersect_kat(const dev::DevScene& sc, int64_t n, int occlusion, const float* rays, const float* nrm,
-                                uint2* gstack, uint32_t nslots, float* out, hipStream_t st);
+                                const int32_t* otri, uint2* gstack, uint32_t nslots, float* out, hipStream_t st);
 hipError_t launch_splat_kat(const dev::DevFrame& fr, int64_t n, const float* p, int32_t* xy, hipStream_t st);
 int frame_kernel_lds_stack();
 int frame_kernel_blocks_per_cu(size_t dyn_lds);
@@ -86,6 +86,7 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess) return fail(BDPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+constexpr int kCounterWords = BDPT_NUM_COUNTERS + 3;  // sums, then the counting pass's 3 maxima (Counts::m)
 constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
 // Short subpaths run the BDPT_SPLIT_CONTINUE build (bdpt_kernels_split.hip): the
 // ST_DEFER step it removes is one loop slot of the ~(rrDepth + 1)^2 / 2 a sample
@@ -147,6 +148,7 @@ struct bdpt_ctx {
     bool tri_tree = false;              // traversal boxes padded (wide_bvh.hpp kTriBoxPad)
     double box_lo[3] = {}, box_hi[3] = {};  // scene bounds (the reference BVH's root box)
     int64_t scene_bytes = 0;
+    int64_t ntri = 0;  // triangles (shade records)
     // work buffers
     unsigned long long* work = nullptr;      // work counter
     unsigned long long* counters = nullptr;  // kCounters
@@ -166,6 +168,9 @@ struct bdpt_ctx {
     uint32_t* pt_ring = nullptr;
     uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28, RR)
     uint32_t* capped = nullptr;   // samples that met the Russian-roulette bounds, per call
+    unsigned long long* diag = nullptr;  // the BDPT frame kernel's timeline (dev::kDiag*)
+    bool diag_pending = false;    // the last call was a BDPT frame render (diag is its)
+    int wall_khz = 100000;        // s_memrealtime rate
     void* pt_dparams = nullptr;
     // single-sample calls: the caller's std::mt19937 state and the splat list
     uint32_t* mt_state = nullptr;  // BDPT_MT19937_WORDS
@@ -193,6 +198,97 @@ static int end_use(bdpt_ctx* c, hipStream_t st) {
     c->last_stream = st;
     c->used = true;
     return BDPT_OK;
+}
+
+// The BSDF records as the kernels read them. A MixtureBSDF with Ks == 0, scale
+// == 1 and a finite exponent >= 0 (so specw == 0) returns DiffuseBSDF's values
+// bit for bit (mixture.h:59-151 against diffuse.h:35-61): eval adds
+// (0 * (n + 2)) * INV_TWOPI * powf(c, n) = +0 (c in [0, 1], so powf is
+// finite) to Kd * INV_PI and multiplies by 1; pdf is pdfPhong * 0 + pdfDiffuse
+// * 1 with a finite pdfPhong; sample takes the diffuse branch (u.x < 0 never
+// holds) with (u.x - 0) / (1 - 0) == u.x. The kernels run it as diffuse, so a
+// wave whose lanes shade both kinds runs one branch instead of two.
+// BDPT_KEEP_MIXTURE=1 keeps the record as loaded (the A/B of DESIGN.md).
+static std::vector<BsdfRecord> device_bsdfs(const std::vector<BsdfRecord>& in) {
+    std::vector<BsdfRecord> out = in;
+    const char* keep = std::getenv("BDPT_KEEP_MIXTURE");
+    if (keep && *keep == '1') return out;
+    for (BsdfRecord& b : out) {
+        const bool ks0 = b.ks[0] == 0.f && b.ks[1] == 0.f && b.ks[2] == 0.f;
+        if (b.kind == BSDF_MIXTURE && ks0 && b.scale == 1.f && b.specw == 0.f && std::isfinite(b.exponent) &&
+            b.exponent >= 0.f)
+            b.kind = BSDF_DIFFUSE;  // type keeps the reference's flags (only its delta bits are read)
+    }
+    return out;
+}
+
+// Near-cull exemption margin of a triangle (cull_near_for, bdpt_path.hpp; DESIGN.md
+// §2 item 5). The frames exempt a query that leaves a surface at |cos| < kGrazeCos
+// to the triangle's GEOMETRIC plane; at run time they only have the interpolated
+// shading normal n_s. Every n_s of the triangle is a normalized positive
+// combination of its corner normals, so it lies in their cone: if each corner
+// normal is within angle th of sgn * n_g (one side of the plane), |n_s - sgn * n_g|
+// <= 2 sin(th / 2) and |dot(d, n_g)| < kGrazeCos implies |dot(d, n_s)| < kGrazeCos +
+// 2 sin(th / 2). The code is that margin in units of 1/64, rounded up (with 1e-5 for
+// the float normalization of n_s); 0 for flat triangles (corner normals parallel to
+// n_g: n_s is then n_g's own direction), 255 (always exempt) for corner normals on
+// both sides of the plane, zero normals or degenerate triangles.
+static uint32_t graze_code(const float* v0, const float* v1, const float* v2, const float* const n[3]) {
+    double e1[3], e2[3];
+    for (int a = 0; a < 3; a++) e1[a] = double(v1[a]) - v0[a], e2[a] = double(v2[a]) - v0[a];
+    double g[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+    const double gl = std::sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+    if (!(gl > 0.0) || !std::isfinite(gl)) return 255u;
+    double worst = 0.0;  // max over corners of 2 sin(th / 2) = |n_k - sgn n_g|
+    int sgn = 0;
+    for (int k = 0; k < 3; k++) {
+        const double nl = std::sqrt(double(n[k][0]) * n[k][0] + double(n[k][1]) * n[k][1] + double(n[k][2]) * n[k][2]);
+        if (!(nl > 0.0) || !std::isfinite(nl)) return 255u;
+        const double c = (n[k][0] * g[0] + n[k][1] * g[1] + n[k][2] * g[2]) / (nl * gl);
+        const int s = c > 0.0 ? 1 : c < 0.0 ? -1 : 0;
+        if (s == 0 || (sgn != 0 && s != sgn)) return 255u;
+        sgn = s;
+        worst = std::max(worst, std::sqrt(std::max(0.0, 2.0 - 2.0 * std::fabs(c))));
+    }
+    if (worst < 1e-9) return 0u;
+    const double code = std::ceil((worst + 1e-5) * 64.0);
+    return code >= 255.0 ? 255u : static_cast<uint32_t>(code);
+}
+
+// The shading records as uploaded (bdpt_types.h kShadeStride): the host five
+// (n0, mat) (n1, shape) (n2, prim) (v1) (v2), + (v0) in the wide layout, with the
+// triangle's graze code in bits 24..31 of the shape word (shape ids < 2^24).
+static std::vector<float4_t> device_shade(const DeviceLayout& L) {
+    const size_t ntri = L.shade.size() / 5;
+    std::vector<float4_t> out(kShadeStride * ntri, float4_t{0.f, 0.f, 0.f, 0.f});
+    for (size_t i = 0; i < ntri; i++) {
+        for (int q = 0; q < 5; q++) out[kShadeStride * i + q] = L.shade[5 * i + q];
+        if (kShadeStride > kShadeV0) out[kShadeStride * i + kShadeV0] = L.tri[3 * i];
+        const float4_t* s = &L.shade[5 * i];
+        const float v0[3] = {L.tri[3 * i].x, L.tri[3 * i].y, L.tri[3 * i].z};
+        const float v1[3] = {s[3].x, s[3].y, s[3].z}, v2[3] = {s[4].x, s[4].y, s[4].z};
+        const float n0[3] = {s[0].x, s[0].y, s[0].z}, n1[3] = {s[1].x, s[1].y, s[1].z}, n2[3] = {s[2].x, s[2].y, s[2].z};
+        const float* const n[3] = {n0, n1, n2};
+        uint32_t shape;
+        std::memcpy(&shape, &s[1].w, 4);
+        shape |= graze_code(v0, v1, v2, n) << 24;
+        std::memcpy(&out[kShadeStride * i + 1].w, &shape, 4);
+    }
+    return out;
+}
+
+// The emitter faces as uploaded: 5 float4 per face (v0 v1 v2 n0 n1 n2, 18 floats)
+// with the face's graze code in the first free word (the first light ray leaves it).
+static std::vector<float4_t> device_emit_tri(const DeviceLayout& L) {
+    std::vector<float4_t> out = L.emit_tri;
+    for (size_t f = 0; f + 5 <= out.size(); f += 5) {
+        float w[20];
+        std::memcpy(w, &out[f], sizeof(w));
+        const float* const n[3] = {w + 9, w + 12, w + 15};
+        const uint32_t code = graze_code(w, w + 3, w + 6, n);
+        std::memcpy(&out[f + 4].z, &code, 4);
+    }
+    return out;
 }
 
 extern "C" {
@@ -227,19 +323,22 @@ int bdpt_scene_export_layout(const bdpt_scene* s, int32_t array, void* dst, int6
                                static_cast<uint32_t>(L.wdepth)};
     const void* src = nullptr;
     size_t n = 0;
+    std::vector<float4_t> tmp4;
+    std::vector<BsdfRecord> tmpb;
     switch (array) {
         case 0: src = L.tri.data(), n = L.tri.size() * 16; break;
-        case 1: src = L.shade.data(), n = L.shade.size() * 16; break;
+        case 1: tmp4 = device_shade(L), src = tmp4.data(), n = tmp4.size() * 16; break;
         case 2: src = L.nodes.data(), n = L.nodes.size() * 16; break;
         case 3: src = L.wnodes.data(), n = L.wnodes.size() * 16; break;
         case 4: src = L.wtri.data(), n = L.wtri.size() * 16; break;
         case 5: src = L.lbox.data(), n = L.lbox.size() * 16; break;
-        case 6: src = L.bsdfs.data(), n = L.bsdfs.size() * sizeof(BsdfRecord); break;
+        case 6: tmpb = device_bsdfs(L.bsdfs), src = tmpb.data(), n = tmpb.size() * sizeof(BsdfRecord); break;
         case 7: src = L.emitters.data(), n = L.emitters.size() * sizeof(EmitterRecord); break;
-        case 8: src = L.emit_tri.data(), n = L.emit_tri.size() * 16; break;
+        case 8: tmp4 = device_emit_tri(L), src = tmp4.data(), n = tmp4.size() * 16; break;
         case 9: src = L.emit_cdf.data(), n = L.emit_cdf.size() * 4; break;
         case 10: src = L.shape_emitter.data(), n = L.shape_emitter.size() * 4; break;
         case 11: src = roots, n = sizeof(roots); break;
+        case 12: src = L.bsdfs.data(), n = L.bsdfs.size() * sizeof(BsdfRecord); break;
         default: return fail(BDPT_ERR_INVALID, "unknown layout array");
     }
     if (dst) {
@@ -335,28 +434,6 @@ int bdpt_device_count(int32_t* count) {
     return BDPT_OK;
 }
 
-// The BSDF records as the kernels read them. A MixtureBSDF with Ks == 0, scale
-// == 1 and a finite exponent >= 0 (so specw == 0) returns DiffuseBSDF's values
-// bit for bit (mixture.h:59-151 against diffuse.h:35-61): eval adds
-// (0 * (n + 2)) * INV_TWOPI * powf(c, n) = +0 (c in [0, 1], so powf is
-// finite) to Kd * INV_PI and multiplies by 1; pdf is pdfPhong * 0 + pdfDiffuse
-// * 1 with a finite pdfPhong; sample takes the diffuse branch (u.x < 0 never
-// holds) with (u.x - 0) / (1 - 0) == u.x. The kernels run it as diffuse, so a
-// wave whose lanes shade both kinds runs one branch instead of two.
-// BDPT_KEEP_MIXTURE=1 keeps the record as loaded (the A/B of DESIGN.md).
-static std::vector<BsdfRecord> device_bsdfs(const std::vector<BsdfRecord>& in) {
-    std::vector<BsdfRecord> out = in;
-    const char* keep = std::getenv("BDPT_KEEP_MIXTURE");
-    if (keep && *keep == '1') return out;
-    for (BsdfRecord& b : out) {
-        const bool ks0 = b.ks[0] == 0.f && b.ks[1] == 0.f && b.ks[2] == 0.f;
-        if (b.kind == BSDF_MIXTURE && ks0 && b.scale == 1.f && b.specw == 0.f && std::isfinite(b.exponent) &&
-            b.exponent >= 0.f)
-            b.kind = BSDF_DIFFUSE;  // type keeps the reference's flags (only its delta bits are read)
-    }
-    return out;
-}
-
 static int upload(bdpt_ctx* c, const void* src, size_t bytes, void** dst) {
     if (bytes == 0) bytes = 16;
     HIP_TRY(hipMalloc(dst, bytes));
@@ -376,6 +453,7 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
                     static_cast<void*>(c->gstack), static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams,
                     static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
                     static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state), static_cast<void*>(c->capped),
+                    static_cast<void*>(c->diag),
                     static_cast<void*>(c->splat_list)})
         if (p) (void)hipFree(p);
     if (c->last_use) (void)hipEventDestroy(c->last_use);
@@ -406,13 +484,11 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     int rc;
     if ((rc = upload(c.get(), L.tri.data(), L.tri.size() * 16, &p))) return rc;
     c->sc.tri = static_cast<const float4*>(p);
+    if (s->host.shape_first.size() >= (size_t(1) << 24))
+        return fail(BDPT_ERR_UNSUPPORTED, "more than 2^24 shapes (the shading record packs the shape id in 24 bits)");
+    c->ntri = static_cast<int64_t>(L.shade.size() / 5);
     {  // the device shade records (bdpt_types.h kShadeStride): the host five + v0, one line each
-        const size_t ntri = L.shade.size() / 5;
-        std::vector<float4_t> dev_shade(kShadeStride * ntri, float4_t{0.f, 0.f, 0.f, 0.f});
-        for (size_t i = 0; i < ntri; i++) {
-            for (int q = 0; q < 5; q++) dev_shade[kShadeStride * i + q] = L.shade[5 * i + q];
-            if (kShadeStride > kShadeV0) dev_shade[kShadeStride * i + kShadeV0] = L.tri[3 * i];
-        }
+        const std::vector<float4_t> dev_shade = device_shade(L);
         if ((rc = upload(c.get(), dev_shade.data(), dev_shade.size() * 16, &p))) return rc;
     }
     c->sc.shade = static_cast<const float4*>(p);
@@ -439,7 +515,10 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     c->sc.bsdf = static_cast<const BsdfRecord*>(p);
     if ((rc = upload(c.get(), L.emitters.data(), L.emitters.size() * sizeof(EmitterRecord), &p))) return rc;
     c->sc.emit = static_cast<const EmitterRecord*>(p);
-    if ((rc = upload(c.get(), L.emit_tri.data(), L.emit_tri.size() * 16, &p))) return rc;
+    {
+        const std::vector<float4_t> dev_etri = device_emit_tri(L);
+        if ((rc = upload(c.get(), dev_etri.data(), dev_etri.size() * 16, &p))) return rc;
+    }
     c->sc.emit_tri = static_cast<const float4*>(p);
     if ((rc = upload(c.get(), L.emit_cdf.data(), L.emit_cdf.size() * 4, &p))) return rc;
     c->sc.emit_cdf = static_cast<const float*>(p);
@@ -503,7 +582,13 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     }
     c->max_depth = s->host.max_depth;
     HIP_TRY(hipMalloc(&c->work, sizeof(unsigned long long)));
-    HIP_TRY(hipMalloc(&c->counters, sizeof(unsigned long long) * BDPT_NUM_COUNTERS));
+    HIP_TRY(hipMalloc(&c->counters, sizeof(unsigned long long) * kCounterWords));
+    HIP_TRY(hipMalloc(&c->diag, sizeof(unsigned long long) * dev::kDiagWords));
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) == hipSuccess && khz > 0)
+            c->wall_khz = khz;
+    }
     HIP_TRY(hipMalloc(&c->sample_out, 16 * sizeof(float)));
     HIP_TRY(hipMalloc(&c->capped, sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->capped, 0, sizeof(uint32_t)));
@@ -556,6 +641,7 @@ static dev::DevFrame make_frame(const bdpt_frame_params* p) {
     fr.inv_spp = 1.f / static_cast<float>(fr.spp);  // IEEE divisions: the bits of the device's rcp_cr
     fr.inv_pixels = 1.f / static_cast<float>(fr.W * fr.H);
     fr.capped = nullptr;  // the context's word, set by the caller
+    fr.diag = nullptr;    // the context's timeline, set by bdpt_render
     return fr;
 }
 
@@ -620,8 +706,11 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     }
     if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kCounterWords, st));
     HIP_TRY(hipMemsetAsync(c->capped, 0, sizeof(uint32_t), st));
+    HIP_TRY(hipMemsetAsync(c->diag, 0, sizeof(unsigned long long) * dev::kDiagWords, st));
+    HIP_TRY(hipMemsetAsync(c->diag + dev::kDiagStart, 0xff, sizeof(unsigned long long), st));
+    fr.diag = c->diag;
     HIP_TRY(hipEventRecord(c->ev0, st));
     int64_t launches = 0;
     if (fr.total_samples > 0) {
@@ -657,6 +746,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     HIP_TRY(hipEventRecord(c->ev1, st));
     if ((rc = end_use(c, st))) return rc;
     c->pending_timing = true;
+    c->diag_pending = true;
     c->stats = bdpt_stats{};
     c->stats.samples = static_cast<int64_t>(fr.total_samples);
     c->stats.launches = launches;
@@ -723,7 +813,7 @@ int bdpt_render_path(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_pa
     std::memcpy(&settings[3], &path->rr_prob, 4);
     if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kCounterWords, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
     if (fr.total_samples > 0)
         HIP_TRY(launch_pt(c->sc, fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
@@ -731,6 +821,7 @@ int bdpt_render_path(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_pa
     HIP_TRY(hipEventRecord(c->ev1, st));
     if ((rc = end_use(c, st))) return rc;
     c->pending_timing = true;
+    c->diag_pending = false;
     c->stats = bdpt_stats{};
     c->stats.samples = static_cast<int64_t>(fr.total_samples);
     c->stats.launches = fr.total_samples > 0 ? 1 : 0;
@@ -775,7 +866,7 @@ int bdpt_render_direct(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direc
     const int32_t settings[8] = {1, -1, 0, 0, d->emitter_samples, d->bsdf_samples, 1, d->sampling_strategy};
     if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, st));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kCounterWords, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
     if (fr.total_samples > 0)
         HIP_TRY(launch_pt(c->sc, fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
@@ -783,6 +874,7 @@ int bdpt_render_direct(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direc
     HIP_TRY(hipEventRecord(c->ev1, st));
     if ((rc = end_use(c, st))) return rc;
     c->pending_timing = true;
+    c->diag_pending = false;
     c->stats = bdpt_stats{};
     c->stats.samples = static_cast<int64_t>(fr.total_samples);
     c->stats.launches = fr.total_samples > 0 ? 1 : 0;
@@ -838,7 +930,7 @@ static int render_pt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const int32
     sc.mt_ring = c->mt_state;  // the sample kernel's generator state (mt_state_u32)
     HIP_TRY(hipMemcpyAsync(c->mt_state, state, sizeof(uint32_t) * BDPT_MT19937_WORDS, hipMemcpyHostToDevice,
                            c->stream));
-    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * BDPT_NUM_COUNTERS, c->stream));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kCounterWords, c->stream));
     HIP_TRY(launch_pt_sample(sc, fr, settings, c->pt_levels, c->pt_ring, c->gstack, r, c->sample_out, c->counters,
                              c->stream, c->pt_dparams));
     float out[4];
@@ -961,6 +1053,20 @@ int bdpt_get_stats(bdpt_ctx* c, bdpt_stats* out) {
         uint32_t capped = 0;
         HIP_TRY(hipMemcpy(&capped, c->capped, sizeof(capped), hipMemcpyDeviceToHost));
         c->stats.capped_samples = capped;
+        unsigned long long mx[3];
+        HIP_TRY(hipMemcpy(mx, c->counters + BDPT_NUM_COUNTERS, sizeof(mx), hipMemcpyDeviceToHost));
+        c->stats.max_light_depth = static_cast<int64_t>(mx[0]);
+        c->stats.max_eye_depth = static_cast<int64_t>(mx[1]);
+        c->stats.max_queries = static_cast<int64_t>(mx[2]);
+        if (c->diag_pending) {
+            unsigned long long d[dev::kDiagWords];
+            HIP_TRY(hipMemcpy(d, c->diag, sizeof(d), hipMemcpyDeviceToHost));
+            const double tick_ms = 1.0 / c->wall_khz;
+            if (d[dev::kDiagStart] != ~0ull && d[dev::kDiagEnd] >= d[dev::kDiagStart])
+                c->stats.span_ms = static_cast<double>(d[dev::kDiagEnd] - d[dev::kDiagStart]) * tick_ms;
+            if (d[dev::kDiagLastClaim] && d[dev::kDiagEnd] >= d[dev::kDiagLastClaim])
+                c->stats.tail_ms = static_cast<double>(d[dev::kDiagEnd] - d[dev::kDiagLastClaim]) * tick_ms;
+        }
         c->pending_timing = false;
     }
     *out = c->stats;
@@ -1014,7 +1120,8 @@ static int render_bdpt_sample(bdpt_ctx* c, const bdpt_frame_params* p, const flo
     if (rc) return rc;
     if ((rc = check_mt_state(state))) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    if ((rc = ensure_lv(c, make_frame(p).lv_max, c->nslots))) return rc;
+    // the sample kernel's one lane uses lane slot 0 of the light-vertex store
+    if ((rc = ensure_lv(c, make_frame(p).lv_max, 1))) return rc;
     // a sample splats at most once per light vertex: rr_depth bounds the list
     // without Russian roulette; with it the list grows on demand (below)
     if ((rc = ensure_sample_buffers(c, std::max(p->rr_depth, 1)))) return rc;
@@ -1181,11 +1288,11 @@ int bdpt_bsdf_type(const bdpt_scene* s, int32_t mat, uint32_t* type, int32_t* ki
 }
 
 int bdpt_intersect(bdpt_ctx* c, int64_t n, const float* rays, int32_t occlusion, bdpt_hit* out) {
-    return bdpt_intersect_from(c, n, rays, nullptr, occlusion, out);
+    return bdpt_intersect_from(c, n, rays, nullptr, nullptr, occlusion, out);
 }
 
-int bdpt_intersect_from(bdpt_ctx* c, int64_t n, const float* rays, const float* origin_normals, int32_t occlusion,
-                        bdpt_hit* out) {
+int bdpt_intersect_from(bdpt_ctx* c, int64_t n, const float* rays, const float* origin_normals,
+                        const int32_t* origin_tris, int32_t occlusion, bdpt_hit* out) {
     static_assert(sizeof(bdpt_hit) == 20 * 4, "bdpt_hit is the kernel's 20-word record");
     if (!c || n < 0 || (n > 0 && (!rays || !out))) return fail(BDPT_ERR_INVALID, "bad argument");
     if (n == 0) return BDPT_OK;
@@ -1193,10 +1300,14 @@ int bdpt_intersect_from(bdpt_ctx* c, int64_t n, const float* rays, const float* 
     int rc;
     if ((rc = begin_use(c, c->stream))) return rc;
     KatBuffers kb;
-    void *dr, *dout, *dn = nullptr;
+    void *dr, *dout, *dn = nullptr, *dt = nullptr;
     const size_t N = static_cast<size_t>(n);
+    if (origin_tris)
+        for (size_t i = 0; i < N; i++)
+            if (origin_tris[i] < -1 || origin_tris[i] >= c->ntri) return fail(BDPT_ERR_INVALID, "origin_tris out of range");
     if ((rc = kat_in(c, kb, rays, 32 * N, &dr)) || (rc = kat_in(c, kb, nullptr, 80 * N, &dout))) return rc;
     if (origin_normals && (rc = kat_in(c, kb, origin_normals, 12 * N, &dn))) return rc;
+    if (origin_normals && origin_tris && (rc = kat_in(c, kb, origin_tris, 4 * N, &dt))) return rc;
     // The interior-box test the frame kernels would use for these origins: without
     // the ambiguity slack when every origin lies within 100 scene diagonals (as
     // for a frame whose camera does, node_slack_needed), with it otherwise.
@@ -1208,7 +1319,8 @@ int bdpt_intersect_from(bdpt_ctx* c, int64_t n, const float* rays, const float* 
     for (int64_t b = 0; b < n; b += c->nslots) {
         const int64_t m = std::min<int64_t>(c->nslots, n - b);
         HIP_TRY(launch_intersect_kat(sc, m, occlusion ? 1 : 0, static_cast<const float*>(dr) + 8 * b,
-                                     dn ? static_cast<const float*>(dn) + 3 * b : nullptr, c->gstack, c->nslots,
+                                     dn ? static_cast<const float*>(dn) + 3 * b : nullptr,
+                                     dt ? static_cast<const int32_t*>(dt) + b : nullptr, c->gstack, c->nslots,
                                      static_cast<float*>(dout) + 20 * b, c->stream));
     }
     HIP_TRY(hipMemcpyAsync(out, dout, 80 * N, hipMemcpyDeviceToHost, c->stream));

@@ -157,6 +157,10 @@ struct DevFrame {
     int32_t depth_cap;  // subpath depth bound: rr_depth under NO_RR; with RR a guard (2^20 bounces)
     int32_t lv_max;     // light vertices a lane slot stores: rr_depth - 1 under NO_RR, more with RR
     uint32_t* capped;   // RR: samples that hit depth_cap or lv_max (the frame is then not the reference's)
+    // frame-kernel timeline (s_memrealtime ticks): [0] first wave start (min), [1]
+    // the claim of the last 64-sample chunk, [2] last wave exit (max) — the end
+    // tail a row shard pays is [2] - [1] (kDiag*)
+    unsigned long long* diag;
     // 1 / spp and 1 / (W * H) as the host's IEEE divisions, the bits the device's correctly
     // rounded reciprocal (rcp_cr) and division give: per-frame constants the shading bodies
     // would otherwise recompute (~10 instructions each) per splat and per sample
@@ -502,10 +506,21 @@ constexpr float kCullNear = BDPT_CULL_NEAR ? 5e-4f : -__builtin_huge_valf();
 // that plane (a grazing ray leaving a surface) the computed t, u, v are rounding
 // noise the reference still accepts (t > 1e-3), so such queries walk without the
 // near cull: every query leaving a surface (a path vertex or the emitter) at
-// |cos| < kGrazeCos to its shading normal. Below it the
+// |cos| < kGrazeCos to its triangle's plane. Below it the
 // t error of a coplanar triangle, ~1.2e-7 |o - v0| / (|cos| sin(corner)), can
 // pass 1e-3 only for triangles with a corner under ~0.35 degrees.
 constexpr float kGrazeCos = 0.02f;
+// The rule is about the origin triangle's geometric plane; the path only holds
+// the interpolated shading normal n_s, so each triangle carries a graze code (top
+// byte of its shading record's shape word, bdpt_capi.cpp graze_code): n_s lies
+// within code / 64 of the geometric normal's direction, and |dot(d, n_s)| <
+// kGrazeCos + code / 64 covers every |dot(d, n_g)| < kGrazeCos. Code 0 (flat
+// triangles: n_s is n_g) leaves the plain test.
+__device__ __forceinline__ int shape_id(int packed) { return packed & 0xffffff; }
+__device__ __forceinline__ bool graze_exempt(f3 d, f3 n, int packed) {
+    const float thr = kGrazeCos + static_cast<float>(static_cast<uint32_t>(packed) >> 24) * 0.015625f;
+    return fabsf(dot(d, n)) < thr;
+}
 enum : int { kSlabMiss = 0, kSlabHit = 1, kSlabAmbiguous = 2 };
 struct RayInv {
     f3 inv;
@@ -684,7 +699,9 @@ __device__ __forceinline__ float cull_far(float best) { return best + fabsf(best
 
 struct Counts {
     uint32_t c[kCounters];
+    uint32_t m[3];  // maxima (counting pass): light-subpath depth, eye-subpath depth, queries per sample
 };
+enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagWords = 4 };
 
 // SIMD-efficiency probe: true on the lowest active lane of the wave only.
 __device__ __forceinline__ bool first_active_lane() {
@@ -1448,7 +1465,7 @@ __device__ __forceinline__ int cdf_sample_lds(const float* cdf_generic, int ncdf
 // Returns the emitter index.
 template <class Rng>
 __device__ __forceinline__ int sample_emitter(const DevScene& sc, Rng& rng, float& emitter_pdf, f3& n, f3& pos,
-                                              float& pos_pdf) {
+                                              float& pos_pdf, int* graze = nullptr) {
     const float u0 = next1(rng);
     uint32_t id = static_cast<uint32_t>(u0 * static_cast<float>(sc.nemit));
     id = id < static_cast<uint32_t>(sc.nemit - 1) ? id : static_cast<uint32_t>(sc.nemit - 1);
@@ -1481,6 +1498,7 @@ __device__ __forceinline__ int sample_emitter(const DevScene& sc, Rng& rng, floa
     pos = (v0 * w + v1 * uv.x) + v2 * uv.y;
     n = normalize((n0 * w + n1 * uv.x) + n2 * uv.y);
     pos_pdf = rcp_cr(e.area);
+    if (graze) *graze = __float_as_int(g.z) << 24;  // the face's graze code (bdpt_capi.cpp device_emit_tri)
     return static_cast<int>(id);
 }
 

@@ -112,6 +112,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     const Stack stk{stack_mem + threadIdx.x, kBlock, kLdsStack, kp.gstack, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
+    cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
     const LightStore ls = light_store(kp.lv, kp.fr.lv_max, blockIdx.x * kBlock + threadIdx.x);
     unsigned long long* const work = kp.work;
     const uint64_t total = kp.fr.total_samples;
@@ -140,6 +141,8 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     float rt = 0.f, ru = 0.f, rv = 0.f;
 #endif
     const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long* const diag = kp.fr.diag;  // the kernel's timeline (DevFrame::diag)
+    if (diag && lane == 0) gmin(diag + kDiagStart, __builtin_amdgcn_s_memrealtime());
     for (;;) {
         // Re-derived every iteration (opaque to the optimiser) so constants are
         // read where they are used instead of being pinned in registers; typed
@@ -172,6 +175,8 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 chunk_n = static_cast<int>(total - base < 64 ? total - base : 64);
                 chunk_pos = 0;
                 global_done = base + 64 >= total;
+                if (global_done && diag && lane == 0)  // the last chunk of the frame (one wave claims it)
+                    diag[kDiagLastClaim] = __builtin_amdgcn_s_memrealtime();
                 int px;
                 chunk_x397 = mt_x397(sample_seed(base + lane, P->fr, px));
 #if BDPT_EYE_SLOTS
@@ -290,6 +295,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     if (lane == 0)  // every sample of the wave has finished: the slots' sums to the framebuffer
         for (int k = 0; k < BDPT_EYE_SLOTS; k++) eye_slot_reset(kp.fb, k, -1);
 #endif
+    if (diag && lane == 0) gmax(diag + kDiagEnd, __builtin_amdgcn_s_memrealtime());
     if (COUNT) {
         if (lane == 0) cnt.c[14] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - clock0);
         flush_counts(cnt, kp.counters);

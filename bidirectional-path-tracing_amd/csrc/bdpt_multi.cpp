@@ -275,13 +275,21 @@ int bdpt_multi_render_host(bdpt_multi* m, const bdpt_frame_params* params, const
     m->stats.reduce_ms = reduce_ms;
     m->stats.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
     m->stats.samples = 0;
+    m->stats.capped_samples = 0;
     for (int i = 0; i < N; i++) {
         bdpt_stats s;
         if ((rc = bdpt_get_stats(m->ctx[i], &s))) return rc;
         m->stats.kernel_ms[i] = s.kernel_ms;
         m->stats.device_samples[i] = s.samples;
         m->stats.samples += s.samples;
+        m->stats.capped_samples += s.capped_samples;
     }
+    // as bdpt_render_host: a Russian-roulette frame in which some sample met the
+    // light-vertex store or the bounce guard is not the reference's image
+    if (params->russian_roulette && !path && !direct && m->stats.capped_samples)
+        return bdpt::set_error(BDPT_ERR_UNSUPPORTED, std::to_string(m->stats.capped_samples) +
+                                                         " samples met the Russian-roulette bounds (light-vertex store / "
+                                                         "bounce guard); the image is not the reference's");
     return BDPT_OK;
 }
 

@@ -302,7 +302,11 @@ __device__ __forceinline__ void eye_slot_reset(float* __restrict__ fb, int k, in
 
 template <bool COUNT>
 __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __restrict__ fb, Counts& cnt) {
-    if (COUNT) cnt.c[7] += L.rng.n;
+    if (COUNT) {
+        cnt.c[7] += L.rng.n;
+        cnt.m[1] = max(cnt.m[1], static_cast<uint32_t>(L.c.depth));
+        cnt.m[2] = max(cnt.m[2], static_cast<uint32_t>(L.c.steps));
+    }
     // rgb[p] += acc * (1 / spp) (renderer.cpp:202), one sample at a time.
     if (!(fr.flags & kFlagNoEyeAccum) && (L.c.Li.x != 0.f || L.c.Li.y != 0.f || L.c.Li.z != 0.f)) {
         const float inv_spp = fr.inv_spp;  // 1.f / spp
@@ -439,14 +443,16 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
         const BsdfRecord& b = bsdf_of(sc, L.h.mat); \
         const bool delta = is_delta(b); \
         const float rrp = rr_on(fr) ? L.c.rr : 1.f; \
-        if (rr_on(fr) && light && !delta && L.c.nl >= fr.lv_max) {  /* the store is full: flag, end the light walk */ \
+        /* the store is full: the vertex would be pushed only if the walk continues (bdpt.h:211-215) */ \
+        const bool full = rr_on(fr) && light && !delta && L.c.nl >= fr.lv_max; \
+        if (light && !delta && !full) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, rrp);  /* the pre-walk state */ \
+        const bool more = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, rrp); \
+        if (full && more) {  /* it would be stored: flag the sample, end the light walk */ \
             gadd(fr.capped, 1u); \
             L.state = ST_DEFER; \
             act = A_ISSUED; \
             break; \
         } \
-        if (light && !delta) store_vertex(ls, L.c.nl, L.h, L.c.tp, L.c.vcm, L.c.vc, rrp);  /* the pre-walk state */ \
-        const bool more = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, rrp); \
         if (!light) { \
             act = more ? A_EYE_NEXT : A_FINISH; \
         } else if (more) { \
@@ -488,6 +494,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
     BDPT_BODY_LIGHT_NEXT
 #endif
     BDPT_ACTION(21, act == A_START_EYE) {  // eyeSubpathWalk prologue (bdpt.h:47-65)
+        if (COUNT && fr.strategy != 2) cnt.m[0] = max(cnt.m[0], static_cast<uint32_t>(L.c.depth));  // the light walk's
         const f3 prim = L.c.Li;  // the primary hit's (t, u, v), kept since resolve(ST_PRIMARY)
         if (fr.strategy == 1) {  // LIGHT_TRACING: Li = Le at the primary hit (bdpt.h:231)
             const int mat = __float_as_int(gld4(sc.shade + kShadeStride * static_cast<size_t>(L.c.prim_tri)).w);
@@ -524,7 +531,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
         if (!is_zero(emission)) {
-            const int eid = shape_emitter_of(sc, L.h.shape);
+            const int eid = shape_emitter_of(sc, shape_id(L.h.shape));
             if (eid >= 0) {  // (the reference asserts otherwise, integrator.cpp:56)
                 const EmitterRecord& e = emitter_of(sc, eid);
                 const float emitterPdf = sc.inv_nemit;  // 1.f / nemit
@@ -557,11 +564,11 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
     } BDPT_END;
     // The emitter sample (4 draws) of lightSubpathWalk (bdpt.h:162-163) and of
     // connectToLight (bdpt.h:376-381): selectEmitter + sampleEmitterPosition.
-    int e_id = 0;
+    int e_id = 0, e_graze = 0;
     float e_pdf = 0.f, e_pos_pdf = 0.f;
     f3 e_n = mk(0.f, 0.f, 0.f), e_p = e_n;
     BDPT_ACTION(23, act == A_START_LIGHT || act == A_NEE) {
-        e_id = sample_emitter(sc, L.rng, e_pdf, e_n, e_p, e_pos_pdf);
+        e_id = sample_emitter(sc, L.rng, e_pdf, e_n, e_p, e_pos_pdf, &e_graze);
     } BDPT_END;
     BDPT_ACTION(24, act == A_START_LIGHT) {  // lightSubpathWalk prologue (bdpt.h:158-182): 6 draws
         const EmitterRecord& e = emitter_of(sc, e_id);
@@ -574,6 +581,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         make_frame(e_n, fs, ft);
         L.ray = Ray{e_p, to_world(fs, ft, e_n, edir), kEpsilon, 3.402823466e+38f};
         L.h.n = e_n;  // the surface the first light ray leaves (cull_near_for); the walk's resolve overwrites L.h
+        L.h.shape = e_graze;  // its graze code (the shape id is not read before the walk's resolve)
         L.c.tp = (ld3(e.radiance) * edir.z) * rcp_cr(emissionPdf);
         L.c.vc = edir.z * rcp_cr(emissionPdf);
         L.c.vcm = div_cr(areaPdf, emissionPdf);
@@ -731,14 +739,14 @@ __device__ __forceinline__ void start_sample(Lane& L, uint64_t s, const DevFrame
 
 __device__ __forceinline__ bool is_shadow_state(uint32_t st) { return st == ST_SPLAT || st == ST_NEE || st == ST_CONN; }
 
-// The near-cull threshold of the lane's pending query (kGrazeCos,
+// The near-cull threshold of the lane's pending query (kGrazeCos, graze_exempt,
 // bdpt_device.hpp): none for a query that leaves the current vertex (or, for the
-// first light-subpath ray, the emitter: A_START_LIGHT puts its normal in L.h.n)
-// nearly parallel to its surface; camera queries keep it.
+// first light-subpath ray, the emitter: A_START_LIGHT puts its normal and face
+// code in L.h) nearly parallel to its triangle's plane; camera queries keep it.
 __device__ __forceinline__ float cull_near_for(const Lane& L) {
     const uint32_t st = L.state;
     if (st == ST_PRIMARY || st == ST_SPLAT) return kCullNear;
-    return fabsf(dot(L.ray.d, L.h.n)) < kGrazeCos ? kNoCullNear : kCullNear;
+    return graze_exempt(L.ray.d, L.h.n, L.h.shape) ? kNoCullNear : kCullNear;
 }
 
 // Applies the result of the lane's pending query (closest hit: leaf-order
@@ -797,11 +805,17 @@ __device__ __forceinline__ void run_deferred(Lane& L, const DevScene& sc, const 
         advance<COUNT>(L, resolve<COUNT>(L, -1, 0.f, 0.f, 0.f, sc, fr, fb, cnt), sc, fr, fb, ls, cnt);
 }
 
+// out: kCounters sums, then the 3 maxima of Counts::m.
 __device__ __forceinline__ void flush_counts(const Counts& cnt, unsigned long long* out) {
     for (int i = 0; i < kCounters; i++) {
         unsigned long long v = cnt.c[i];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if ((threadIdx.x & 63) == 0 && v) gadd(out + i, v);
+    }
+    for (int i = 0; i < 3; i++) {
+        uint32_t v = cnt.m[i];
+        for (int off = 32; off > 0; off >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), off)));
+        if ((threadIdx.x & 63) == 0 && v) gmax(out + kCounters + i, static_cast<unsigned long long>(v));
     }
 }
 

@@ -40,6 +40,12 @@ __device__ __forceinline__ uint32_t gadd(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ unsigned long long gadd(unsigned long long* p, unsigned long long v) {
     return __hip_atomic_fetch_add((gu64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void gmax(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_fetch_max((gu64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gmin(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_fetch_min((gu64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // ---------------------------------------------------------------- float3
 struct f3 {

@@ -74,10 +74,12 @@ __global__ __launch_bounds__(kKatBlock) void triangle_kat_kernel(int64_t n, cons
 // p[3], frameNs.n[3], frameNg.n[3], wo[3], leaf-order triangle index (int bits).
 // nrm (optional, 3 per ray): the normal of the surface the ray leaves, for the
 // frame kernels' near-cull rule (cull_near_for: a zero normal = a camera
-// origin); without it no box is near-culled.
+// origin), otri (optional) the triangle of that surface, whose graze code widens
+// the threshold as in the frames; without nrm no box is near-culled.
 __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, int64_t n, int occlusion,
                                                                  const float* __restrict__ rays,
                                                                  const float* __restrict__ nrm,
+                                                                 const int32_t* __restrict__ otri,
                                                                  uint2* __restrict__ gstack, uint32_t nslots,
                                                                  float* __restrict__ out) {
     __shared__ uint2 stack_mem[kLdsStack * kKatBlock];
@@ -94,7 +96,9 @@ __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, i
     if (nrm) {
         const f3 sn = mk(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]);
         const bool camera = sn.x == 0.f && sn.y == 0.f && sn.z == 0.f;
-        near = (camera || !(fabsf(dot(ray.d, sn)) < kGrazeCos)) ? kCullNear : kNoCullNear;
+        const int ot = otri ? otri[i] : -1;
+        const int code = ot >= 0 ? __float_as_int(gld4(sc.shade + kShadeStride * static_cast<size_t>(ot) + 1).w) : 0;
+        near = (camera || !graze_exempt(ray.d, sn, code)) ? kCullNear : kNoCullNear;
     }
     const int res = traverse<false, false>(sc, ray, occlusion != 0, stk, t, u, v, cnt, near);
     float* o = out + 20 * i;
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, i
     const f3 v0 = xyz(gld4(sc.tri + 3 * static_cast<size_t>(res))), v1 = xyz(gld4(sh + 3)), v2 = xyz(gld4(sh + 4));
     const f3 ng = normalize(cross(v1 - v0, v2 - v0));
     o[0] = __int_as_float(1), o[2] = u, o[3] = v;
-    o[4] = __int_as_float(h.shape), o[5] = __int_as_float(__float_as_int(gld4(sh + 2).w)), o[6] = __int_as_float(h.mat);
+    o[4] = __int_as_float(shape_id(h.shape)), o[5] = __int_as_float(__float_as_int(gld4(sh + 2).w)), o[6] = __int_as_float(h.mat);
     o[7] = h.p.x, o[8] = h.p.y, o[9] = h.p.z;
     o[10] = h.n.x, o[11] = h.n.y, o[12] = h.n.z;
     o[13] = ng.x, o[14] = ng.y, o[15] = ng.z;
@@ -150,11 +154,11 @@ hipError_t launch_triangle_kat(int64_t n, const float* rays, const float* verts,
     return hipGetLastError();
 }
 hipError_t launch_intersect_kat(const dev::DevScene& sc, int64_t n, int occlusion, const float* rays, const float* nrm,
-                                uint2* gstack, uint32_t nslots, float* out, hipStream_t st) {
+                                const int32_t* otri, uint2* gstack, uint32_t nslots, float* out, hipStream_t st) {
     if (n > 0)
         hipLaunchKernelGGL(dev::intersect_kat_kernel, kat_grid(n), dim3(dev::kKatBlock),
-                           4 * static_cast<size_t>(sc.lds_words), st, sc, n, occlusion, rays, nrm, gstack, nslots,
-                           out);
+                           4 * static_cast<size_t>(sc.lds_words), st, sc, n, occlusion, rays, nrm, otri, gstack,
+                           nslots, out);
     return hipGetLastError();
 }
 hipError_t launch_splat_kat(const dev::DevFrame& fr, int64_t n, const float* p, int32_t* xy, hipStream_t st) {

@@ -518,7 +518,7 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
             return pt_advance(L, PS_DIRE, zero, P, slot);  // no recursion: indirectEstimator stays 0
         }
         case PQ_DIRE: {  // path.h:134-151
-            if (hit && vis.shape == L.e_shape) {
+            if (hit && shape_id(vis.shape) == L.e_shape) {
                 const f3 Li = emission_of(sc, vis.mat);
                 const BsdfRecord& b = bsdf_of(sc, L.h.mat);
                 const float a2s = L.e_cos * rcp_cr(L.e_d2);
@@ -535,7 +535,7 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
         case PQ_DIRB: {  // path.h:162-184
             if (hit) {
                 const f3 Li = emission_of(sc, vis.mat);
-                const int eid = shape_emitter_of(sc, vis.shape);
+                const int eid = shape_emitter_of(sc, shape_id(vis.shape));
                 if (!is_zero(Li) && eid >= 0) {
                     const EmitterRecord& e = emitter_of(sc, eid);
                     const float emitterPdf = 1.f / static_cast<float>(sc.nemit);
@@ -592,7 +592,7 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
                 return pt_advance(L, PS_DI_EMIT, zero, P, slot);
             }
             // solid angle / MIS: the emitter's shape hit first, or nothing hit and the ray meets the sphere
-            const bool lit = hit ? vis.shape == e.shape : ray_sphere_hit(L.ray, ld3(e.center), e.radius);
+            const bool lit = hit ? shape_id(vis.shape) == e.shape : ray_sphere_hit(L.ray, ld3(e.center), e.radius);
             if (lit) {
                 if (st == DI_SOLID_ANGLE) {  // direct.h:283-306
                     const f3 c = (ld3(e.radiance) * bsdf_eval(b, L.e_wil, L.h.wo)) * rcp_cr(L.e_apdf);
@@ -613,7 +613,7 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
                 if (S.direct == DI_BSDF) {  // direct.h:253-256: Le * brdfCosTheta * (1.0 / pdf)
                     L.ind = L.ind + (Le * L.b_f) * rcp_cr(L.b_pdf);
                 } else if (!is_zero(Le)) {  // direct.h:390-414
-                    const int eid = shape_emitter_of(sc, vis.shape);
+                    const int eid = shape_emitter_of(sc, shape_id(vis.shape));
                     if (eid >= 0) {
                         const EmitterRecord& e = emitter_of(sc, eid);
                         const f3 dd = L.h.p - ld3(e.center);
@@ -649,6 +649,7 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
     const int lane = threadIdx.x & 63;
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
+    cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
     PtLane L;
     L.busy = false;
     L.q = PQ_NONE;
@@ -695,7 +696,8 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
         // PT_SHADE_READY of the wave have one, then advance together.
         if (L.busy && !tracing && !has_res) {
             if (COUNT) cnt.c[0]++;
-            ri = ray_inv(L.ray, kCullNear);
+            // no near cull for a query leaving the vertex nearly parallel to its triangle (cull_near_for)
+            ri = ray_inv(L.ray, (L.q != PQ_PRIMARY && graze_exempt(L.ray.d, L.h.n, L.h.shape)) ? kNoCullNear : kCullNear);
             if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root (bvh.h:277, :287)
                 res = -1, rt = L.ray.max_t, ru = rv = 0.f;
                 has_res = true;
@@ -761,6 +763,7 @@ __global__ __launch_bounds__(64) void pt_sample_kernel(const PtParams* __restric
     const Stack stk{stack_mem, 64, kLdsStack, P.gstack, 1, 0};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
+    cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
     // Value-initialised: with a partly uninitialised lane record this one-lane
     // build returned garbage in Li.x (0x5a5a5a5a) although every field is
     // assigned before it is read on the reference's control flow (measured on

@@ -141,6 +141,12 @@ typedef struct {
                                does not have - more than max(255, rr_depth - 1) stored light vertices, or
                                2^20 bounces in one subpath (> 0 means the frame is not the reference's,
                                and bdpt_render_host fails) */
+    double span_ms;         /* BDPT frame kernel, device clock: first wave start -> last wave exit */
+    double tail_ms;         /* BDPT frame kernel, device clock: the frame's last 64-sample chunk claimed ->
+                               last wave exit (the end tail a persistent grid pays per launch) */
+    int64_t max_light_depth; /* counting pass (BDPT_FLAG_COUNT) maxima over the samples: light-subpath */
+    int64_t max_eye_depth;   /* depth, eye-subpath depth, */
+    int64_t max_queries;     /* ray queries of one sample */
 } bdpt_stats;
 
 const char* bdpt_last_error(void);
@@ -208,13 +214,17 @@ typedef struct {
  * copies it; the caller's arrays may be freed afterwards. BDPT_ERR_INVALID with a
  * message when it is inconsistent. */
 int bdpt_scene_create(const bdpt_scene_desc* desc, bdpt_scene** out);
-/* The scene's device arrays as uploaded by bdpt_ctx_create, for
+/* The scene's device arrays as uploaded by bdpt_ctx_create (the
+ * same transforms: shade records widened with v0 and the triangle's near-cull
+ * graze code in the shape word's top byte, mixture records with Ks = 0 as
+ * diffuse, emitter faces with their graze code), for
  * checking that two ingest paths agree bit for bit: 0 tri, 1 shade, 2 nodes (the
  * reference's binary tree), 3 wnodes, 4 wtri, 5 lbox, 6 BSDF records, 7 emitter
  * records, 8 emitter faces, 9 emitter CDFs, 10 shape -> emitter, 11 roots / tree
- * sizes (uint32 root_link, wroot_link, wmax_stack, wdepth). *bytes = the array's
- * size; dst may be NULL (size only), else it must hold *bytes on entry. */
-#define BDPT_LAYOUT_ARRAYS 12
+ * sizes (uint32 root_link, wroot_link, wmax_stack, wdepth), 12 the BSDF records
+ * as ingested (before the upload's mixture -> diffuse rewrite). *bytes = the
+ * array's size; dst may be NULL (size only), else it must hold *bytes on entry. */
+#define BDPT_LAYOUT_ARRAYS 13
 int bdpt_scene_export_layout(const bdpt_scene* scene, int32_t array, void* dst, int64_t* bytes);
 /* Camera constants: worldToCamera, cameraToWorld, cameraToClip, NDCToScreen
  * (column-major) then invWidth, invHeight, tan(fov/2), aspect, forward.xyz,
@@ -350,6 +360,8 @@ typedef struct {
     int64_t samples;   /* camera samples over all devices */
     double kernel_ms[BDPT_MAX_DEVICES];      /* per device, HIP events of its render kernel */
     int64_t device_samples[BDPT_MAX_DEVICES];
+    int64_t capped_samples;  /* Russian roulette: bdpt_stats.capped_samples summed over the devices; a
+                                non-zero sum fails bdpt_multi_render_host as it fails bdpt_render_host */
 } bdpt_multi_stats;
 int bdpt_multi_create(const bdpt_scene* scene, int32_t ndevices, const int32_t* devices, bdpt_multi** out);
 int bdpt_multi_destroy(bdpt_multi* multi);
@@ -394,12 +406,15 @@ typedef struct {
  * with it otherwise. */
 int bdpt_intersect(bdpt_ctx* ctx, int64_t n, const float* rays, int32_t occlusion, bdpt_hit* out);
 /* The same with the frame kernels' near-cull rule: origin_normals (n x 3) is the
- * normal of the surface each ray leaves (a path vertex's shading normal, the
- * emitter's normal), zero for a camera origin. bdpt_intersect (origin_normals
- * NULL) culls no box for lying close to the origin; the frames skip such boxes
- * unless the query leaves its surface at |cos| < 0.02. */
-int bdpt_intersect_from(bdpt_ctx* ctx, int64_t n, const float* rays, const float* origin_normals, int32_t occlusion,
-                        bdpt_hit* out);
+ * normal of the surface each ray leaves (a path vertex's interpolated shading
+ * normal, the emitter point's normal), zero for a camera origin; origin_tris
+ * (n, may be NULL = all -1) the triangle that surface is (bdpt_hit.tri order),
+ * -1 for none. bdpt_intersect (origin_normals NULL) culls no box for lying close
+ * to the origin; the frames skip such boxes unless the query leaves its surface
+ * at |cos| < 0.02 to the triangle's geometric plane, tested as |dot(d, n_s)| <
+ * 0.02 + the triangle's normal-cone margin. */
+int bdpt_intersect_from(bdpt_ctx* ctx, int64_t n, const float* rays, const float* origin_normals,
+                        const int32_t* origin_tris, int32_t occlusion, bdpt_hit* out);
 /* BDPTIntegrator::splatToImagePlane (bdpt.h:485-496) of points p (n x 3) for the
  * camera and image of params: xy = n x 2 (the reference's int truncation). */
 int bdpt_splat_to_image_plane(bdpt_ctx* ctx, const bdpt_frame_params* params, int64_t n, const float* p,

@@ -98,6 +98,10 @@ LARGE_FRAMEBUFFERS = {
     "L0_caustic_512x512_spp256_rows8": ("caustic", 512, 512, 256, 8, 31, 64, 32),
     "L1_caustic_1024x1024_spp1024_rows2": ("caustic", 1024, 1024, 1024, 8, 300, 512, 32),
     "L2_synth1m_2048x2048_spp512_rows2": ("synth1m", 2048, 2048, 512, 8, 700, 1024, 64),
+    # configs[2] at its own spp (HardLight, rrDepth 2: the short-subpath build)
+    "L3_hardlight_512x512_spp1024_rows8": ("hardlight", 512, 512, 1024, 2, 17, 64, 32),
+    # the bench workload with Russian roulette (the reference's NO_RR = 0 build, ref_bdpt_rr)
+    "L4_caustic_rr_512x512_spp256_rows8": ("caustic", 512, 512, 256, 8, 45, 64, 32, 1),
 }
 
 SCENE_DUMPS = {"cbox_low": (64, 64), "caustic": (512, 512), "hardlight": (512, 512), "hardlight_mirror": (512, 512),
@@ -209,14 +213,16 @@ def main() -> None:
                                                      mean_rgb=[float(x) for x in fb.reshape(-1, 3).mean(0)],
                                                      ref_seconds=info["seconds"])
         print(name, manifest["direct_framebuffers"][name]["sha256"][:16], info)
-    for name, (scene, W, H, spp, rr, off, stride, blk) in LARGE_FRAMEBUFFERS.items():
+    for name, entry in LARGE_FRAMEBUFFERS.items():
         if only and name not in only:
             continue
+        scene, W, H, spp, rr, off, stride, blk = entry[:8]
+        russian_roulette = entry[8] if len(entry) > 8 else 0
         toml = os.path.join(tmp, name + ".toml")
         with open(toml, "w") as f:
             f.write(variants.toml_text(scene, W, H, spp, rr))
         out = os.path.join(tmp, name + ".f32")
-        r = subprocess.run([REF, "render", toml, str(W), str(H), str(spp), "--rr", str(rr), "--out", out,
+        r = subprocess.run([REF_RR if russian_roulette else REF, "render", toml, str(W), str(H), str(spp), "--rr", str(rr), "--out", out,
                             "--row-offset", str(off), "--row-stride", str(stride), "--threads", "8"],
                            capture_output=True, text=True, check=True)
         info = json.loads(r.stdout.strip().splitlines()[-1])
@@ -228,6 +234,7 @@ def main() -> None:
         manifest.setdefault("large_framebuffers", dict(old.get("large_framebuffers", {})))
         manifest["large_framebuffers"][name] = dict(scene=scene, width=W, height=H, spp=spp, rr_depth=rr,
                                                     row_offset=off, row_stride=stride, block=blk,
+                                                    russian_roulette=russian_roulette,
                                                     samples=info["samples"], threads=8,
                                                     sha256_rows=sha(fb[rows].tobytes()),
                                                     frame_sum=[float(x) for x in blocks.sum((0, 1))],

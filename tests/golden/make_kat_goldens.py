@@ -180,10 +180,11 @@ def _normalize(v):
     return (v / np.linalg.norm(v, axis=-1, keepdims=True)).astype(f32)
 
 
-def _surface_points(rng, tri, idx):
+def _surface_points(rng, tri, idx, nrm=None):
     """Points on triangles idx as the path computes hit points (shade_hit /
     SurfaceInteraction: (v0 w + v1 u) + v2 v in float32), with a share exactly on
-    edges and vertices."""
+    edges and vertices. With nrm (the corner normals, [ntri, 9]) also the
+    interpolated shading normals there (normalize((n0 w + n1 u) + n2 v), float32)."""
     n = idx.size
     u = rng.random(n).astype(f32)
     v = (rng.random(n) * (1 - u)).astype(f32)
@@ -196,21 +197,31 @@ def _surface_points(rng, tri, idx):
     u[c], v[c] = 0, 0
     w = (f32(1) - u - v).astype(f32)
     v0, v1, v2 = tri[idx, 0:3], tri[idx, 3:6], tri[idx, 6:9]
-    return ((v0 * w[:, None] + v1 * u[:, None]) + v2 * v[:, None]).astype(f32)
+    p = ((v0 * w[:, None] + v1 * u[:, None]) + v2 * v[:, None]).astype(f32)
+    if nrm is None:
+        return p
+    n0, n1, n2 = nrm[idx, 0:3], nrm[idx, 3:6], nrm[idx, 6:9]
+    sn = ((n0 * w[:, None] + n1 * u[:, None]) + n2 * v[:, None]).astype(f32)
+    sn = (sn / np.sqrt(np.sum(sn.astype(f32) * sn, 1, keepdims=True, dtype=f32))).astype(f32)
+    return p, sn
 
 
 def adversarial_rays(scene, n, seed):
     """Rays chosen where the product traversal's exactness argument is thinnest
     (DESIGN.md §2 items 5-6): the computed hit of Moller-Trumbore near |det| = 1e-8,
     ties between triangles sharing an edge or a vertex, origins on surfaces, and
-    origins beyond 100 scene diagonals. Returns (rays [n, 8] float32, kind [n],
-    the normal of the triangle a ray leaves [n, 3] (0 for camera / free / far origins))."""
+    origins beyond 100 scene diagonals, and (kinds 6, 7) grazing rays leaving the
+    curved mesh, whose interpolated shading normal is not the triangle's plane
+    normal. Returns (rays [n', 8] float32, kind [n'], the geometric normal of the
+    triangle a ray leaves [n', 3] (0 for camera / free / far origins), that
+    triangle [n'] (-1: none) and the shading normal the path holds there [n', 3])."""
     sys.path.insert(0, os.path.join(REPO, "bidirectional-path-tracing_amd"))
     import bdpt_amd
 
     rng = np.random.default_rng(seed)
     tf, ti, nf, _ = bdpt_amd.Scene(variants.obj_path(scene)).export()
     tri = tf[:, :9].astype(f32)
+    cnrm = tf[:, 9:18].astype(f32)
     e1, e2 = tri[:, 3:6] - tri[:, 0:3], tri[:, 6:9] - tri[:, 0:3]
     cr = np.cross(e1.astype(np.float64), e2.astype(np.float64))
     area = 0.5 * np.linalg.norm(cr, axis=1)
@@ -225,11 +236,18 @@ def adversarial_rays(scene, n, seed):
     curved = np.flatnonzero(ti[:, 0] == shapes[np.argmax(counts)])  # the tessellated sphere(s)
     FLT_MAX = 3.402823466e38
     k = n // 6
-    out, kind, onrm = [], [], []
+    out, kind, onrm, otri, osn = [], [], [], [], []
 
-    def add(o, d, mn, mx, tag, nrm=None):
+    def add(o, d, mn, mx, tag, nrm=None, tri_idx=None, sn=None):
+        ok = np.isfinite(o).all(1) & np.isfinite(d).all(1)  # degenerate triangles of a generated mesh
+        if not ok.all():
+            o, d = o[ok], d[ok]
+            mn, mx = (mn if np.isscalar(mn) else mn[ok]), (mx if np.isscalar(mx) else mx[ok])
+            nrm, tri_idx, sn = (None if x is None else np.asarray(x)[ok] for x in (nrm, tri_idx, sn))
         m = o.shape[0]
         onrm.append(np.zeros((m, 3), f32) if nrm is None else np.asarray(nrm, f32))
+        otri.append(np.full(m, -1, np.int32) if tri_idx is None else np.asarray(tri_idx, np.int32))
+        osn.append(np.zeros((m, 3), f32) if sn is None else np.asarray(sn, f32))
         out.append(np.concatenate([o, _normalize(d), np.broadcast_to(np.float32(mn), (m, 1)) if np.isscalar(mn)
                                    else mn[:, None], np.broadcast_to(np.float32(mx), (m, 1)) if np.isscalar(mx)
                                    else mx[:, None]], 1).astype(f32))
@@ -237,7 +255,7 @@ def adversarial_rays(scene, n, seed):
 
     # 0: grazing continuation rays from points on the large triangles, |sin| from 0 to 1e-2
     idx = rng.choice(big, k)
-    o = _surface_points(rng, tri, idx)
+    o, sn = _surface_points(rng, tri, idx, cnrm)
     t1 = _normalize(e1[idx])
     t2 = _normalize(np.cross(ng[idx], t1))
     phi = rng.random(k) * 2 * np.pi
@@ -245,16 +263,16 @@ def adversarial_rays(scene, n, seed):
                        k) * rng.choice([-1, 1], k)
     d = t1 * np.cos(phi)[:, None] + t2 * np.sin(phi)[:, None] + ng[idx] * delta[:, None]
     h = rng.choice([0.0, 0.0, 1e-7, -1e-7, 1e-6, -1e-6, 1e-5, 1e-4], k)
-    add((o + ng[idx] * h[:, None]).astype(f32), d, 1e-8, FLT_MAX, 0, ng[idx])
+    add((o + ng[idx] * h[:, None]).astype(f32), d, 1e-8, FLT_MAX, 0, ng[idx], idx, sn)
     # 1: grazing shadow segments between two points of the same large triangle (visibilityQuery)
     idx = rng.choice(big, k)
-    a, b = _surface_points(rng, tri, idx), _surface_points(rng, tri, idx)
+    (a, sn), b = _surface_points(rng, tri, idx, cnrm), _surface_points(rng, tri, idx)
     lift = rng.choice([0.0, 1e-7, 1e-5, 1e-3], k)[:, None] * ng[idx]
     a, b = (a + lift).astype(f32), (b + lift).astype(f32)
     dd = (b - a).astype(f32)
     dist = np.sqrt((dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1]) + dd[:, 2] * dd[:, 2]).astype(f32)
     keep = dist > 1e-4
-    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 1, ng[idx][keep])
+    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 1, ng[idx][keep], idx[keep], sn[keep])
     # 2: rays through the curved mesh's vertices and edges (ties between neighbours, silhouettes)
     idx = rng.choice(curved, k)
     w = rng.choice(4, k)
@@ -266,13 +284,13 @@ def adversarial_rays(scene, n, seed):
     add(o, tgt - o, 1e-8, FLT_MAX, 2)
     # 3: continuation rays from surface points of any triangle, both hemispheres, near-tangent included
     idx = rng.integers(0, tri.shape[0], k)
-    o = _surface_points(rng, tri, idx)
+    o, sn = _surface_points(rng, tri, idx, cnrm)
     d = rng.normal(size=(k, 3))
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     flat = rng.random(k) < 0.3
     d[flat] -= ng[idx][flat] * np.sum(d[flat] * ng[idx][flat], 1, keepdims=True) * (1 - rng.choice(
         [1e-6, 1e-4, 1e-2], flat.sum()))[:, None]
-    add(o, d, 1e-8, FLT_MAX, 3, ng[idx])
+    add(o, d, 1e-8, FLT_MAX, 3, ng[idx], idx, sn)
     # 4: origins 100 - 10000 scene diagonals away, aimed at surface points (the slack-test regime)
     dirn = rng.normal(size=(k, 3))
     dirn /= np.linalg.norm(dirn, axis=1, keepdims=True)
@@ -284,19 +302,48 @@ def adversarial_rays(scene, n, seed):
     # 5: shadow segments between surface points of any two triangles
     m = n - 5 * k
     ia = rng.integers(0, tri.shape[0], m)
-    a = _surface_points(rng, tri, ia)
+    a, sn = _surface_points(rng, tri, ia, cnrm)
     b = _surface_points(rng, tri, rng.integers(0, tri.shape[0], m))
     dd = (b - a).astype(f32)
     dist = np.sqrt((dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1]) + dd[:, 2] * dd[:, 2]).astype(f32)
     keep = dist > 1e-4
-    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 5, ng[ia][keep])
-    return np.concatenate(out), np.concatenate(kind), np.concatenate(onrm)
+    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 5, ng[ia][keep], ia[keep], sn[keep])
+    # 6: grazing continuation rays leaving the curved mesh: |cos| to the
+    # triangle's plane from 0 to 0.1, while the interpolated shading normal the path
+    # tests against (cull_near_for) is tilted from that plane's normal
+    idx = rng.choice(curved, k)
+    o, sn = _surface_points(rng, tri, idx, cnrm)
+    t1 = _normalize(e1[idx])
+    t2 = _normalize(np.cross(ng[idx], t1))
+    phi = rng.random(k) * 2 * np.pi
+    delta = rng.choice([0.0, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 3e-3, 1e-2, 0.015, 0.019, 0.021, 0.03, 0.05, 0.1],
+                       k) * rng.choice([-1, 1], k)
+    d = t1 * np.cos(phi)[:, None] + t2 * np.sin(phi)[:, None] + ng[idx] * delta[:, None]
+    h = rng.choice([0.0, 0.0, 1e-7, -1e-7, 1e-6, -1e-6], k)
+    add((o + ng[idx] * h[:, None]).astype(f32), d, 1e-8, FLT_MAX, 6, ng[idx], idx, sn)
+    # 7: grazing shadow segments from the curved mesh along its triangles' planes
+    idx = rng.choice(curved, k)
+    a, sn = _surface_points(rng, tri, idx, cnrm)
+    t1 = _normalize(e1[idx])
+    t2 = _normalize(np.cross(ng[idx], t1))
+    phi = rng.random(k) * 2 * np.pi
+    delta = rng.choice([0.0, 1e-6, 1e-4, 1e-2, 0.019, 0.03, 0.1], k) * rng.choice([-1, 1], k)
+    d = _normalize(t1 * np.cos(phi)[:, None] + t2 * np.sin(phi)[:, None] + ng[idx] * delta[:, None])
+    ln = np.exp(rng.uniform(np.log(1e-3), np.log(2.0), k))
+    b = (a + d * ln[:, None]).astype(f32)
+    dd = (b - a).astype(f32)
+    dist = np.sqrt((dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1]) + dd[:, 2] * dd[:, 2]).astype(f32)
+    keep = dist > 1e-4
+    add(a[keep], dd[keep], 1e-8, (dist[keep] - f32(1e-5)).astype(f32), 7, ng[idx][keep], idx[keep], sn[keep])
+    return (np.concatenate(out), np.concatenate(kind), np.concatenate(onrm), np.concatenate(otri),
+            np.concatenate(osn))
 
 
 def adversarial_fixture(scene, n, seed):
-    rays, kind, onrm = adversarial_rays(scene, n, seed)
+    rays, kind, onrm, otri, osn = adversarial_rays(scene, n, seed)
     out = kat(toml(scene), 64, 64, "intersect", rays, 21)
     np.savez_compressed(os.path.join(HERE, f"kat_adversarial_{scene}.npz"), rays=rays, kind=kind, onrm=onrm,
+                        otri=otri, osn=osn,
                         hit=out[:, 0].astype(np.int8), t=out[:, 1], u=out[:, 2], v=out[:, 3],
                         shape=out[:, 4].view(np.int32), prim=out[:, 5].view(np.int32),
                         occluded=out[:, 20].astype(np.int8))

@@ -120,17 +120,22 @@ def test_gpu_intersect_adversarial_rays_match_reference(scene):
     hit (acceptance, t, u, v, shape, prim) and occlusion bit for bit against the
     reference's AcceleratorBVH; the in-scene batches run the frames' slack-free
     interior test, the far batch and the mixed batch the slack test (far origins
-    themselves walk the reference's tree), each without the near cull and with
-    the frames' near-cull rule."""
+    themselves walk the reference's tree), each without the near cull, with the
+    near cull skipped at |cos| < 0.02 to the origin triangle's plane normal, and
+    with the frames' own rule (cull_near_for): the interpolated shading normal
+    the path holds at the origin plus that triangle's graze code. Kinds 6 and 7
+    leave the curved mesh nearly parallel to a triangle whose shading normal is
+    tilted from its plane normal (1.7 k such rays in Caustic graze
+    the plane at |cos| < 0.02 while |cos| to the shading normal is >= 0.02)."""
     g = kat(f"kat_adversarial_{scene}")
     it = integrator(scene)
-    rays, kind, onrm = g["rays"], g["kind"], g["onrm"]
+    rays, kind, onrm, otri, osn = g["rays"], g["kind"], g["onrm"], g["otri"], g["osn"]
     far = kind == 4
-    # without the near cull (bdpt_intersect), then with the frames' rule given the
-    # surfaces the rays leave (bdpt_intersect_from: near cull unless |cos| < 0.02)
-    for sel, nrm in ((~far, None), (far, None), (np.ones_like(far), None), (~far, onrm[~far]),
-                     (np.ones_like(far), onrm)):
-        h = it.intersect(rays[sel], origin_normals=nrm)
+    every = np.ones_like(far)
+    cases = ((~far, None, None), (far, None, None), (every, None, None), (~far, onrm[~far], None),
+             (every, onrm, None), (~far, osn[~far], otri[~far]), (every, osn, otri))
+    for sel, nrm, tris in cases:
+        h = it.intersect(rays[sel], origin_normals=nrm, origin_tris=tris)
         hit = g["hit"][sel].astype(np.int32)
         bad = np.flatnonzero(h["hit"] != hit)
         assert bad.size == 0, f"{bad.size} acceptance mismatches, kinds {np.bincount(kind[sel][bad])}"
@@ -139,7 +144,7 @@ def test_gpu_intersect_adversarial_rays_match_reference(scene):
         assert same_bits(h["v"][k], g["v"][sel][k])
         assert np.array_equal(h["shape_id"][k], g["shape"][sel][k]) and np.array_equal(h["prim_id"][k],
                                                                                           g["prim"][sel][k])
-        occ = it.intersect(rays[sel], occlusion=True, origin_normals=nrm)
+        occ = it.intersect(rays[sel], occlusion=True, origin_normals=nrm, origin_tris=tris)
         bad = np.flatnonzero(occ["hit"] != g["occluded"][sel].astype(np.int32))
         assert bad.size == 0, f"{bad.size} occlusion mismatches, kinds {np.bincount(kind[sel][bad])}"
 

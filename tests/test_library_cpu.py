@@ -207,3 +207,45 @@ def test_scene_desc_is_validated():
         with pytest.raises(bdpt_amd.BdptError, match="descriptor|texture"):
             bdpt_amd.Scene.from_desc(bad)
             pytest.fail(what)
+
+
+@pytest.mark.parametrize("scene_name", ["caustic", "hardlight", "synth1m"])
+def test_graze_codes_cover_the_shading_normal_tilt(scene_name):
+    """The near-cull exemption (cull_near_for) is about the
+    origin triangle's geometric plane, tested at run time against the
+    interpolated shading normal n_s with a per-triangle margin (the graze code,
+    top byte of the uploaded shape word, bdpt_capi.cpp graze_code). Check on the
+    uploaded records: flat triangles (corner normals along the plane normal) carry
+    code 0, and for every triangle |n_s - sgn n_g| <= code / 64 at random
+    barycentric points (float32 interpolation and normalization as shade_hit)."""
+    s = bdpt_amd.Scene(variants.obj_path(scene_name))
+    rec = np.frombuffer(s.export_layout("shade"), np.float32).reshape(-1, 8, 4)
+    words = rec.view(np.uint32)
+    code = (words[:, 1, 3] >> 24).astype(np.int64)
+    shape = words[:, 1, 3] & 0xFFFFFF
+    tf, ti, _, _ = s.export()
+    assert np.array_equal(shape, ti[:, 0].astype(np.uint32))  # the shape id survives the packing
+    n = rec[:, 0:3, 0:3].astype(np.float64)
+    v0, v1, v2 = rec[:, 5, :3].astype(np.float64), rec[:, 3, :3].astype(np.float64), rec[:, 4, :3].astype(np.float64)
+    g = np.cross(v1 - v0, v2 - v0)
+    gl = np.linalg.norm(g, axis=1)
+    ok = gl > 0
+    g[ok] /= gl[ok, None]
+    nn = n / np.maximum(np.linalg.norm(n, axis=2, keepdims=True), 1e-300)
+    cos = np.einsum("tkc,tc->tk", nn, g)
+    flat = ok & (np.abs(np.abs(cos) - 1.0) < 1e-12).all(1) & ((cos > 0).all(1) | (cos < 0).all(1))
+    assert (code[flat] == 0).all()
+    assert (code[~ok] == 255).all()
+    rng = np.random.default_rng(3)
+    u = rng.random((code.size, 8)).astype(np.float32)
+    v = (rng.random((code.size, 8)) * (1 - u)).astype(np.float32)
+    w = (np.float32(1) - u - v).astype(np.float32)
+    nf = rec[:, 0:3, 0:3]
+    sn = ((nf[:, None, 0] * w[..., None] + nf[:, None, 1] * u[..., None]) + nf[:, None, 2] * v[..., None])
+    sn = (sn / np.linalg.norm(sn, axis=2, keepdims=True)).astype(np.float64)
+    sgn = np.sign(cos[:, :1])
+    tilt = np.linalg.norm(sn - sgn[:, :, None] * g[:, None, :], axis=2).max(1)
+    sel = ok & (code < 255)
+    assert (tilt[sel] <= code[sel] / 64.0 + 1e-6).all(), float((tilt[sel] - code[sel] / 64.0).max())
+    if scene_name != "synth1m":
+        assert (code > 0).any() and (code == 0).any()  # the sphere is smooth, the walls are flat
