@@ -210,7 +210,23 @@ def issue_roofline(deep: dict, kernel_s: float) -> dict | None:
     return out
 
 
+def heartbeat(period: float = 30.0) -> None:
+    """A line on stderr every `period` s while the process runs (a Russian-roulette
+    frame is one kernel of a minute or more: without output it looks hung)."""
+    import threading
+
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"[bench] running, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main() -> None:
+    heartbeat()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)

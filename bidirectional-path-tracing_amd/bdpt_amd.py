@@ -170,12 +170,12 @@ class _Stats(ctypes.Structure):
                 ("counters", ctypes.c_int64 * len(COUNTER_NAMES)),  # BDPT_NUM_COUNTERS
                 ("capped_samples", ctypes.c_int64), ("span_ms", ctypes.c_double), ("tail_ms", ctypes.c_double),
                 ("max_light_depth", ctypes.c_int64), ("max_eye_depth", ctypes.c_int64),
-                ("max_queries", ctypes.c_int64)]
+                ("max_queries", ctypes.c_int64), ("schedule_errors", ctypes.c_int64)]
 
 
 # Sources that make up the frame kernels' code objects: their hash stamps the
 # profiles (PMC passes) so bench.py only reuses a measurement of the same kernel.
-KERNEL_SOURCES = ("csrc/bdpt_kernels.hip", "csrc/bdpt_kernels_split.hip", "csrc/bdpt_path.hpp", "csrc/bdpt_device.hpp", "csrc/device_math.hpp",
+KERNEL_SOURCES = ("csrc/bdpt_kernels.hip", "csrc/bdpt_kernels_split.hip", "csrc/bdpt_kernels_dq.hip", "csrc/bdpt_path.hpp", "csrc/bdpt_device.hpp", "csrc/device_math.hpp",
                   "csrc/bdpt_types.h", "Makefile")
 
 
@@ -721,7 +721,7 @@ class BDPTIntegrator:
         return dict(kernel_ms=s.kernel_ms, samples=s.samples, launches=s.launches,
                     counters=dict(zip(COUNTER_NAMES, list(s.counters))), capped_samples=s.capped_samples,
                     span_ms=s.span_ms, tail_ms=s.tail_ms, max_light_depth=s.max_light_depth,
-                    max_eye_depth=s.max_eye_depth, max_queries=s.max_queries,
+                    max_eye_depth=s.max_eye_depth, max_queries=s.max_queries, schedule_errors=s.schedule_errors,
                     kernel=(lib().bdpt_last_kernel(self._h) or b"").decode())
 
     def synchronize(self) -> None:

@@ -60,6 +60,12 @@ hipError_t launch_frame_split(const dev::DevScene& sc, const dev::DevFrame& fr, 
                               uint2* gstack, uint32_t nslots, unsigned long long* work, unsigned long long* counters,
                               int grid, hipStream_t stream, void* dparams);
 int frame_kernel_blocks_per_cu_split(size_t dyn_lds);
+// bdpt_kernels_dq.hip: the lane-decoupled build (connection tasks run by other lanes)
+size_t frame_params_bytes_dq();
+hipError_t launch_frame_dq(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, float* evbuf,
+                           uint32_t ev_max, uint2* gstack, uint32_t nslots, unsigned long long* work,
+                           unsigned long long* counters, int grid, hipStream_t stream, void* dparams);
+int frame_kernel_blocks_per_cu_dq(size_t dyn_lds);
 size_t pt_params_bytes();
 int pt_blocks_per_cu(size_t dyn_lds);
 hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8], float* fb,
@@ -95,6 +101,13 @@ constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227
 // HardLight rrDepth 2 / 3 / 4 / 5: +12.5 / +4.4 / +1.2 / -0.2 %).
 // BDPT_SPLIT_MAX_RR overrides the threshold (0: never).
 constexpr int kSplitMaxRrDepth = 3;
+// The lane-decoupled build (bdpt_kernels_dq.hip) for frames without Russian
+// roulette, rrDepth <= 28 and the BSDF table in LDS; BDPT_DQ=1 / 0 forces it on / off.
+constexpr bool kDqDefault = false;
+static bool use_dq_build() {
+    const char* e = std::getenv("BDPT_DQ");
+    return e ? *e == '1' : kDqDefault;
+}
 static bool use_split_build(int rr_depth) {
     const char* e = std::getenv("BDPT_SPLIT_MAX_RR");  // read per render (tests force either build)
     return rr_depth <= (e ? std::atoi(e) : kSplitMaxRrDepth);
@@ -108,7 +121,10 @@ constexpr int kMaxRrDepth = 1024;  // beyond 28 the megakernel continues MT19937
 // meets either is counted (bdpt_stats.capped_samples) and the host render fails
 // rather than return a different image.
 constexpr int kRrLightVerts = 255;
-constexpr int kRrDepthGuard = 1 << 20;
+// A Caustic light subpath trapped in the glass sphere by total internal reflection
+// runs for millions of bounces (the oracle over a 512^2 x 256 frame: 2.7 M light /
+// 2.1 M eye bounces in one sample); the guard sits an order of magnitude above.
+constexpr int kRrDepthGuard = 1 << 25;
 }  // namespace
 
 // Error reporting shared with the other C-ABI translation units (exr_io.cpp, toml_config.cpp).
@@ -149,6 +165,10 @@ struct bdpt_ctx {
     double box_lo[3] = {}, box_hi[3] = {};  // scene bounds (the reference BVH's root box)
     int64_t scene_bytes = 0;
     int64_t ntri = 0;  // triangles (shade records)
+    uint32_t lds_words_base = 0;  // dynamic LDS words without the emitter faces / CDFs
+    float* ev = nullptr;          // the decoupled build's eye-vertex records
+    size_t ev_floats = 0;
+    void* dq_dparams = nullptr;
     // work buffers
     unsigned long long* work = nullptr;      // work counter
     unsigned long long* counters = nullptr;  // kCounters
@@ -259,6 +279,8 @@ static uint32_t graze_code(const float* v0, const float* v1, const float* v2, co
 // (n0, mat) (n1, shape) (n2, prim) (v1) (v2), + (v0) in the wide layout, with the
 // triangle's graze code in bits 24..31 of the shape word (shape ids < 2^24).
 static std::vector<float4_t> device_shade(const DeviceLayout& L) {
+    const char* gz = std::getenv("BDPT_GRAZE_CODES");  // "0": every code 0 (the plain |cos| < 0.02 test; A/B only)
+    const bool codes = !(gz && *gz == '0');
     const size_t ntri = L.shade.size() / 5;
     std::vector<float4_t> out(kShadeStride * ntri, float4_t{0.f, 0.f, 0.f, 0.f});
     for (size_t i = 0; i < ntri; i++) {
@@ -271,7 +293,7 @@ static std::vector<float4_t> device_shade(const DeviceLayout& L) {
         const float* const n[3] = {n0, n1, n2};
         uint32_t shape;
         std::memcpy(&shape, &s[1].w, 4);
-        shape |= graze_code(v0, v1, v2, n) << 24;
+        if (codes) shape |= graze_code(v0, v1, v2, n) << 24;
         std::memcpy(&out[kShadeStride * i + 1].w, &shape, 4);
     }
     return out;
@@ -453,7 +475,7 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
                     static_cast<void*>(c->gstack), static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams,
                     static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
                     static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state), static_cast<void*>(c->capped),
-                    static_cast<void*>(c->diag),
+                    static_cast<void*>(c->diag), static_cast<void*>(c->ev), c->dq_dparams,
                     static_cast<void*>(c->splat_list)})
         if (p) (void)hipFree(p);
     if (c->last_use) (void)hipEventDestroy(c->last_use);
@@ -568,6 +590,7 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
         c->sc.lds_etri_off = c->sc.lds_ecdf_off = dev::kNoLds;
         c->sc.n_etri = static_cast<int32_t>(L.emit_tri.size() / 5);
         c->sc.n_ecdf = static_cast<int32_t>(L.emit_cdf.size());
+        c->lds_words_base = c->sc.lds_words;
         const uint32_t etri = c->sc.lds_words, ecdf = up4(etri + 20u * static_cast<uint32_t>(c->sc.n_etri));
         const uint32_t with = up4(ecdf + static_cast<uint32_t>(c->sc.n_ecdf));
         auto blocks = [&](uint32_t words) {
@@ -593,6 +616,7 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     HIP_TRY(hipMalloc(&c->capped, sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->capped, 0, sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&c->dparams, frame_params_bytes()));
+    HIP_TRY(hipMalloc(&c->dq_dparams, frame_params_bytes_dq()));
     // Persistent grid: exactly the resident blocks (no co-residency is assumed:
     // the work queue has no inter-block waits, extra blocks would just queue).
     const size_t dyn = 4 * static_cast<size_t>(c->sc.lds_words);
@@ -696,13 +720,24 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     if (hbm && (p->rr_depth > kLazyRrDepth || rr))
         return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 or Russian roulette with BSDF records in HBM (too many "
                                           "materials for the LDS table) is not built");
-    if ((rc = ensure_lv(c, fr.lv_max, c->nslots))) return rc;
+    const bool dq = !rr && p->rr_depth <= kLazyRrDepth && !hbm && use_dq_build();
+    // the decoupled build keeps two record buffers per lane slot (light and eye vertices, the eye records 128 B)
+    if ((rc = ensure_lv(c, fr.lv_max, dq ? 2 * c->nslots : c->nslots))) return rc;
+    if (dq) {
+        const size_t evn = static_cast<size_t>(p->rr_depth) * 32 * 2 * c->nslots;
+        if (evn > c->ev_floats) {
+            if (c->ev) HIP_TRY(hipFree(c->ev));
+            c->ev = nullptr;
+            HIP_TRY(hipMalloc(&c->ev, evn * sizeof(float)));
+            c->ev_floats = evn;
+        }
+    }
     dev::DevScene sc = c->sc;
     sc.node_slack = node_slack_needed(c, eye, 1);
     if (p->rr_depth > kLazyRrDepth || rr) {  // draws past 226: the lanes' MT19937 rings
         if (!c->mt_ring) HIP_TRY(hipMalloc(&c->mt_ring, sizeof(uint32_t) * 624 * static_cast<size_t>(c->nslots)));
         sc.mt_ring = c->mt_ring;
-        sc.mt_ring_stride = c->nslots;
+        sc.mt_ring_stride = 1;  // slot-major blocks of 624 words (DevScene::mt_ring)
     }
     if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
@@ -730,6 +765,21 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
             HIP_TRY(launch_frame_hbm(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
                                      c->dparams));
             c->last_kernel = "bdpt_frame_kernel_hbm";
+        } else if (dq) {
+            // the build's static LDS leaves less room: the emitter faces stay in HBM
+            // when keeping them in LDS would cost a resident block
+            dev::DevScene sdq = sc;
+            int blocks = frame_kernel_blocks_per_cu_dq(4 * static_cast<size_t>(sdq.lds_words));
+            if (sdq.lds_etri_off != dev::kNoLds &&
+                frame_kernel_blocks_per_cu_dq(4 * static_cast<size_t>(c->lds_words_base)) > blocks) {
+                sdq.lds_etri_off = sdq.lds_ecdf_off = dev::kNoLds;
+                sdq.lds_words = c->lds_words_base;
+                blocks = frame_kernel_blocks_per_cu_dq(4 * static_cast<size_t>(sdq.lds_words));
+            }
+            const int grid = std::min(c->grid, c->cus * blocks);
+            HIP_TRY(launch_frame_dq(sdq, fr, fb, c->lv, c->ev, static_cast<uint32_t>(p->rr_depth), c->gstack, c->nslots,
+                                    c->work, c->counters, grid, st, c->dq_dparams));
+            c->last_kernel = "bdpt_frame_kernel_dq";
         } else if (use_split_build(p->rr_depth)) {  // never more resident blocks than the slots allocated
             const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_split(
                                                            4 * static_cast<size_t>(c->sc.lds_words)));
@@ -1066,6 +1116,7 @@ int bdpt_get_stats(bdpt_ctx* c, bdpt_stats* out) {
                 c->stats.span_ms = static_cast<double>(d[dev::kDiagEnd] - d[dev::kDiagStart]) * tick_ms;
             if (d[dev::kDiagLastClaim] && d[dev::kDiagEnd] >= d[dev::kDiagLastClaim])
                 c->stats.tail_ms = static_cast<double>(d[dev::kDiagEnd] - d[dev::kDiagLastClaim]) * tick_ms;
+            c->stats.schedule_errors = static_cast<int64_t>(d[dev::kDiagErrors]);
         }
         c->pending_timing = false;
     }
@@ -1101,10 +1152,13 @@ int bdpt_render_host(bdpt_ctx* c, const bdpt_frame_params* p, float* fb_host) {
     if ((rc = bdpt_render(c, p, c->tmp_fb, c->stream))) return rc;
     HIP_TRY(hipMemcpyAsync(fb_host, c->tmp_fb, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (p->russian_roulette) {
+    {
         bdpt_stats st;
         if ((rc = bdpt_get_stats(c, &st))) return rc;
-        if (st.capped_samples)
+        if (st.schedule_errors)
+            return fail(BDPT_ERR_HIP, std::to_string(st.schedule_errors) + " connection tasks named no record "
+                                                                           "(lane-decoupled build)");
+        if (p->russian_roulette && st.capped_samples)
             return fail(BDPT_ERR_UNSUPPORTED, std::to_string(st.capped_samples) +
                                                   " samples met the Russian-roulette bounds (light-vertex store / "
                                                   "bounce guard); the image is not the reference's");

@@ -65,8 +65,11 @@ struct DevScene {
     // costing a resident block (host decision); kNoLds otherwise
     uint32_t lds_etri_off, lds_ecdf_off;
     int32_t n_etri, n_ecdf;
-    // MT19937 continuation ring of the megakernel's lanes (rrDepth > 28): word k
-    // of lane slot s at mt_ring[k * mt_ring_stride + s]; null otherwise
+    // MT19937 continuation ring of the megakernel's lanes (rrDepth > 28, Russian
+    // roulette): word k of lane slot s at mt_ring[s * 624 + k] (one 2.5 KB block per
+    // slot: a lane's draws touch one page, not 624 pages a slot-count stride apart —
+    // a Russian-roulette subpath trapped in glass draws millions of them alone);
+    // mt_ring_stride is the word stride within a block (1); null otherwise
     uint32_t* mt_ring;
     uint32_t mt_ring_stride;
     // The scene box grown by 100 scene diagonals: a query whose origin lies
@@ -154,7 +157,7 @@ struct DevFrame {
     uint32_t flags;
     uint64_t total_samples;  // nrows * W * spp
     int32_t rr_mode;    // 1: NO_RR = 0 (Russian roulette past rr_depth; the bdpt_kernels_rr.hip build)
-    int32_t depth_cap;  // subpath depth bound: rr_depth under NO_RR; with RR a guard (2^20 bounces)
+    int32_t depth_cap;  // subpath depth bound: rr_depth under NO_RR; with RR a guard (2^25 bounces)
     int32_t lv_max;     // light vertices a lane slot stores: rr_depth - 1 under NO_RR, more with RR
     uint32_t* capped;   // RR: samples that hit depth_cap or lv_max (the frame is then not the reference's)
     // frame-kernel timeline (s_memrealtime ticks): [0] first wave start (min), [1]
@@ -334,7 +337,7 @@ __device__ BDPT_NOINLINE uint32_t mt_u32_long(LazyMT& r) {
     if (!ring) return mt_next_u32(r);  // unreachable (host check)
     const uint32_t st = g_scene_lds[2];
     const uint32_t seed = r.n == 227 ? mt_seed_from(r.a0, 227) : 0u;
-    return mt_ring_step(r, seed, ring + (blockIdx.x * blockDim.x + threadIdx.x), st);
+    return mt_ring_step(r, seed, ring + static_cast<size_t>(blockIdx.x * blockDim.x + threadIdx.x) * 624, st);
 }
 
 #endif
@@ -517,8 +520,12 @@ constexpr float kGrazeCos = 0.02f;
 // kGrazeCos + code / 64 covers every |dot(d, n_g)| < kGrazeCos. Code 0 (flat
 // triangles: n_s is n_g) leaves the plain test.
 __device__ __forceinline__ int shape_id(int packed) { return packed & 0xffffff; }
+#ifndef BDPT_GRAZE
+#define BDPT_GRAZE 1  // 0: the plain |cos| < kGrazeCos test (A/B only; not exact on smooth meshes)
+#endif
 __device__ __forceinline__ bool graze_exempt(f3 d, f3 n, int packed) {
-    const float thr = kGrazeCos + static_cast<float>(static_cast<uint32_t>(packed) >> 24) * 0.015625f;
+    const float thr = BDPT_GRAZE ? kGrazeCos + static_cast<float>(static_cast<uint32_t>(packed) >> 24) * 0.015625f
+                                 : kGrazeCos;
     return fabsf(dot(d, n)) < thr;
 }
 enum : int { kSlabMiss = 0, kSlabHit = 1, kSlabAmbiguous = 2 };
@@ -701,7 +708,7 @@ struct Counts {
     uint32_t c[kCounters];
     uint32_t m[3];  // maxima (counting pass): light-subpath depth, eye-subpath depth, queries per sample
 };
-enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagWords = 4 };
+enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagErrors = 3, kDiagWords = 4 };
 
 // SIMD-efficiency probe: true on the lowest active lane of the wave only.
 __device__ __forceinline__ bool first_active_lane() {

@@ -56,6 +56,12 @@ constexpr int kBlock = 256;
 #ifndef BDPT_SHADE_READY
 #define BDPT_SHADE_READY 48  // lanes with a finished query that trigger the wave's shading step
 #endif
+#ifndef BDPT_TAIL_SHADE
+#define BDPT_TAIL_SHADE 0  // once a wave has no samples left to claim: 1 shade at 1 ready lane, 2 at 3/4 of its busy lanes
+#endif
+#ifndef BDPT_EXPRESS_DEPTH
+#define BDPT_EXPRESS_DEPTH 512  // Russian-roulette build: a subpath this deep puts its wave in express mode (below)
+#endif
 #ifndef BDPT_ROOT_LDS
 #define BDPT_ROOT_LDS 1  // 1: the traversal root and its interior children in LDS, tested when a walk begins (RootLds; measured +1.6 %)
 #endif
@@ -140,9 +146,20 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     int res = -1;
     float rt = 0.f, ru = 0.f, rv = 0.f;
 #endif
+    // Russian roulette: a subpath trapped in glass by total internal reflection
+    // runs for millions of bounces, one bounce per shading step of
+    // its wave. A wave holding a subpath past BDPT_EXPRESS_DEPTH stops refilling
+    // and shades as soon as any lane has a result, so once its other samples end
+    // the trapped lane advances one bounce per walk instead of one per shared
+    // shading step (the frame cannot end before it does).
+    bool long_walk = false;
     const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
-    unsigned long long* const diag = kp.fr.diag;  // the kernel's timeline (DevFrame::diag)
-    if (diag && lane == 0) gmin(diag + kDiagStart, __builtin_amdgcn_s_memrealtime());
+#ifndef BDPT_DIAG
+#define BDPT_DIAG 1  // 0: no timeline stamps (A/B only)
+#endif
+    // the kernel's timeline (DevFrame::diag), read through the parameter block
+    // where it is stamped (a pointer held across the loop costs SGPR spills)
+    if (BDPT_DIAG && kp.fr.diag && lane == 0) gmin(kp.fr.diag + kDiagStart, __builtin_amdgcn_s_memrealtime());
     for (;;) {
         // Re-derived every iteration (opaque to the optimiser) so constants are
         // read where they are used instead of being pinned in registers; typed
@@ -151,12 +168,13 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         uint64_t pa = (uint64_t)(ConstKParams)kpp;
         asm volatile("" : "+s"(pa));
         const KParams* P = (const KParams*)(ConstKParams)pa;
+        const bool express = BDPT_RR == 1 && __ballot(long_walk) != 0;  // wave-uniform
 #if BDPT_SEED_CHUNK
         // Refill idle lanes from the wave's chunk of 64 consecutive samples. A
         // chunk is claimed with one atomic and the seeding recurrence of all its
         // samples (mt_x397) runs once with every lane busy, instead of once per
         // refill with only the refilled lanes doing useful work.
-        while (!exhausted) {
+        while (!exhausted && !express) {
             const uint64_t idle = __ballot(L.state == ST_IDLE);
             if (!idle) break;
             if (chunk_pos >= chunk_n) {
@@ -175,8 +193,8 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 chunk_n = static_cast<int>(total - base < 64 ? total - base : 64);
                 chunk_pos = 0;
                 global_done = base + 64 >= total;
-                if (global_done && diag && lane == 0)  // the last chunk of the frame (one wave claims it)
-                    diag[kDiagLastClaim] = __builtin_amdgcn_s_memrealtime();
+                if (BDPT_DIAG && global_done && lane == 0 && P->fr.diag)  // the frame's last chunk (one wave claims it)
+                    P->fr.diag[kDiagLastClaim] = __builtin_amdgcn_s_memrealtime();
                 int px;
                 chunk_x397 = mt_x397(sample_seed(base + lane, P->fr, px));
 #if BDPT_EYE_SLOTS
@@ -251,7 +269,11 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const uint64_t tr = __ballot(tracing);
             if (!tr) break;
             const uint64_t ready = __ballot(has_res);
-            if (__popcll(ready) >= BDPT_SHADE_READY) break;
+            if (__popcll(ready) >= (express ? 1
+                                    : BDPT_TAIL_SHADE == 1 && exhausted ? 1
+                                    : BDPT_TAIL_SHADE == 2 && exhausted ? max(1, (__popcll(tr | ready) * 3) >> 2)
+                                                                        : BDPT_SHADE_READY))
+                break;
 #if BDPT_TRAV_SPLIT
             // Lanes at a leaf and lanes at an interior node step in alternate
             // iterations (whichever group is larger in the sense of the ratio
@@ -281,6 +303,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const uint32_t act = resolve<COUNT>(L, res, rt, ru, rv, P->sc, P->fr, P->fb, cnt);
             if (COUNT && first_active_lane()) cnt.c[20] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - r0);
             advance<COUNT>(L, act, P->sc, P->fr, P->fb, ls, cnt);
+            if (BDPT_RR == 1) long_walk = L.state != ST_IDLE && L.c.depth > BDPT_EXPRESS_DEPTH;
         }
         if (COUNT && first_active_lane()) {
             const uint64_t c2 = __builtin_amdgcn_s_memtime();
@@ -295,7 +318,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     if (lane == 0)  // every sample of the wave has finished: the slots' sums to the framebuffer
         for (int k = 0; k < BDPT_EYE_SLOTS; k++) eye_slot_reset(kp.fb, k, -1);
 #endif
-    if (diag && lane == 0) gmax(diag + kDiagEnd, __builtin_amdgcn_s_memrealtime());
+    if (BDPT_DIAG && lane == 0 && kpp->fr.diag) gmax(kpp->fr.diag + kDiagEnd, __builtin_amdgcn_s_memrealtime());
     if (COUNT) {
         if (lane == 0) cnt.c[14] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - clock0);
         flush_counts(cnt, kp.counters);

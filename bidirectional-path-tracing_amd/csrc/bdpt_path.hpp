@@ -20,7 +20,7 @@ constexpr uint32_t kFlagNoEyeAccum = 0x100u;  // single-sample API: Li is return
 // Safety bound on the queries of one sample: a legal sample issues at most D
 // light-walk rays, D camera splats, D eye-walk rays and, per eye vertex, one
 // light sample plus D - 1 connections: < (D + 3)(D + 1) for rrDepth D. With
-// Russian roulette the walks are bounded by DevFrame::depth_cap (2^20 bounces,
+// Russian roulette the walks are bounded by DevFrame::depth_cap (2^25 bounces,
 // each eye vertex with at most lv_max connections): 2^30 is beyond any legal sample.
 __device__ __forceinline__ int max_steps_per_sample(int rr_depth) { return (rr_depth + 3) * (rr_depth + 1) + 64; }
 
@@ -581,7 +581,10 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         make_frame(e_n, fs, ft);
         L.ray = Ray{e_p, to_world(fs, ft, e_n, edir), kEpsilon, 3.402823466e+38f};
         L.h.n = e_n;  // the surface the first light ray leaves (cull_near_for); the walk's resolve overwrites L.h
-        L.h.shape = e_graze;  // its graze code (the shape id is not read before the walk's resolve)
+#ifndef BDPT_EMIT_GRAZE
+#define BDPT_EMIT_GRAZE 1  // 0: the emitter face's graze code is not used (A/B only)
+#endif
+        if (BDPT_EMIT_GRAZE) L.h.shape = e_graze;  // its graze code (the shape id is not read before the walk's resolve)
         L.c.tp = (ld3(e.radiance) * edir.z) * rcp_cr(emissionPdf);
         L.c.vc = edir.z * rcp_cr(emissionPdf);
         L.c.vcm = div_cr(areaPdf, emissionPdf);

@@ -653,8 +653,8 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
     PtLane L;
     L.busy = false;
     L.q = PQ_NONE;
-    L.rng.ring = P.ring + slot;
-    L.rng.stride = P.nslots;
+    L.rng.ring = P.ring + static_cast<size_t>(slot) * 624;  // slot-major (DevScene::mt_ring)
+    L.rng.stride = 1;
     const uint64_t total = P.fr.total_samples;
     bool exhausted = false;
     const TravScene tsc = trav_scene(P.sc);

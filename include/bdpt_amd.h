@@ -139,7 +139,7 @@ typedef struct {
     int64_t counters[BDPT_NUM_COUNTERS];
     int64_t capped_samples; /* Russian roulette: samples of the last call that met a bound the reference
                                does not have - more than max(255, rr_depth - 1) stored light vertices, or
-                               2^20 bounces in one subpath (> 0 means the frame is not the reference's,
+                               2^25 bounces in one subpath (> 0 means the frame is not the reference's,
                                and bdpt_render_host fails) */
     double span_ms;         /* BDPT frame kernel, device clock: first wave start -> last wave exit */
     double tail_ms;         /* BDPT frame kernel, device clock: the frame's last 64-sample chunk claimed ->
@@ -147,6 +147,8 @@ typedef struct {
     int64_t max_light_depth; /* counting pass (BDPT_FLAG_COUNT) maxima over the samples: light-subpath */
     int64_t max_eye_depth;   /* depth, eye-subpath depth, */
     int64_t max_queries;     /* ray queries of one sample */
+    int64_t schedule_errors; /* lane-decoupled build: connection tasks whose descriptor named no record
+                                (skipped; any non-zero count is a bug, and bdpt_render_host fails) */
 } bdpt_stats;
 
 const char* bdpt_last_error(void);

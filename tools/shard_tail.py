@@ -28,17 +28,20 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     full = None
     for n in ns:
-        ms = []
+        ms, tails = [], []
         for rep in range(3):
             fb.zero_()
             integ.render_device(fb.data_ptr(), stream, row_offset=0, row_stride=n)
-            ms.append(integ.stats()["kernel_ms"])
+            st = integ.stats()
+            ms.append(st["kernel_ms"])
+            tails.append(st.get("tail_ms", 0.0))
         t = min(ms[1:])
+        tail = min(tails[1:])
         if n == 1:
             full = t
         ideal = full / n if full else float("nan")
-        print(f"row_stride {n}: kernel {t:.2f} ms, full/{n} = {ideal:.2f} ms, efficiency {ideal / t:.3f}",
-              flush=True)
+        print(f"row_stride {n}: kernel {t:.2f} ms, full/{n} = {ideal:.2f} ms, efficiency {ideal / t:.3f}, "
+              f"end tail {tail:.2f} ms", flush=True)
 
 
 if __name__ == "__main__":
