@@ -92,7 +92,7 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess) return fail(BDPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int kCounterWords = BDPT_NUM_COUNTERS + 3;  // sums, then the counting pass's 3 maxima (Counts::m)
+constexpr int kCounterWords = BDPT_NUM_COUNTERS + 3 + 4;  // sums, the counting pass's 3 maxima (Counts::m), Counts::q
 constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
 // Short subpaths run the BDPT_SPLIT_CONTINUE build (bdpt_kernels_split.hip): the
 // ST_DEFER step it removes is one loop slot of the ~(rrDepth + 1)^2 / 2 a sample
@@ -627,7 +627,8 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     // right children; 4-wide: the host-computed bound), the part beyond the
     // kernel's LDS entries in HBM.
     const int depth = std::max(s->host.max_depth + 2, L.wmax_stack + 1);
-    const size_t spill_mega = static_cast<size_t>(std::max(0, depth - frame_kernel_lds_stack())) * c->nslots;
+    c->sc.gdepth = static_cast<uint32_t>(std::max(1, depth - frame_kernel_lds_stack()));  // per slot (DevScene::gdepth)
+    const size_t spill_mega = static_cast<size_t>(c->sc.gdepth) * c->nslots;
     HIP_TRY(hipMalloc(&c->gstack, sizeof(uint2) * std::max<size_t>(1, spill_mega)));
     *out = c.release();
     return BDPT_OK;
@@ -1108,6 +1109,9 @@ int bdpt_get_stats(bdpt_ctx* c, bdpt_stats* out) {
         c->stats.max_light_depth = static_cast<int64_t>(mx[0]);
         c->stats.max_eye_depth = static_cast<int64_t>(mx[1]);
         c->stats.max_queries = static_cast<int64_t>(mx[2]);
+        unsigned long long sq[4];
+        HIP_TRY(hipMemcpy(sq, c->counters + BDPT_NUM_COUNTERS + 3, sizeof(sq), hipMemcpyDeviceToHost));
+        for (int i = 0; i < 4; i++) c->stats.sched[i] = static_cast<int64_t>(sq[i]);
         if (c->diag_pending) {
             unsigned long long d[dev::kDiagWords];
             HIP_TRY(hipMemcpy(d, c->diag, sizeof(d), hipMemcpyDeviceToHost));

@@ -79,7 +79,16 @@ struct DevScene {
     // more than the traversal tree's padding.
     float near_lo[3], near_hi[3];
     uint32_t q_ok;  // qnodes present: the BDPT_QNODES kernels walk the 4-wide tree (else the binary one)
+    // traversal-stack overflow entries per lane slot (the entries past the LDS ones):
+    // slot s's entries are the gstack block [s * gdepth, (s + 1) * gdepth) — one
+    // lane's deep stack touches one page (a subpath trapped in the Caustic glass
+    // sphere walks nested boxes alone for millions of queries)
+    uint32_t gdepth;
 };
+// The overflow block of lane slot `slot` (Stack::gbl with nslots = 1, slot = 0).
+__device__ __forceinline__ uint2* stack_block(uint2* gstack, uint32_t gdepth, uint32_t slot) {
+    return gstack + static_cast<size_t>(slot) * gdepth;
+}
 constexpr uint32_t kNoLds = 0xffffffffu;
 constexpr uint32_t kLdsHdr = 4;  // LDS header words: mt_ring (2 words), mt_ring_stride, unused
 
@@ -665,7 +674,7 @@ struct Stack {
     uint2* lds;
     int stride;
     int nlds;    // entries held in LDS
-    uint2* gbl;  // entry k >= nlds at gbl[(k - nlds) * nslots + slot]
+    uint2* gbl;  // entry k >= nlds at gbl[(k - nlds) * nslots + slot] (the frame kernels: the slot's block, nslots 1)
     uint32_t nslots, slot;
     __device__ __forceinline__ void put(int k, uint32_t link, float tn) const {
         const u32x2 e = {link, __float_as_uint(tn)};
@@ -707,6 +716,7 @@ __device__ __forceinline__ float cull_far(float best) { return best + fabsf(best
 struct Counts {
     uint32_t c[kCounters];
     uint32_t m[3];  // maxima (counting pass): light-subpath depth, eye-subpath depth, queries per sample
+    uint32_t q[4];  // lane-decoupled build: task-phase wave clocks, ring tasks popped, tasks without a ray, own tasks
 };
 enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagErrors = 3, kDiagWords = 4 };
 

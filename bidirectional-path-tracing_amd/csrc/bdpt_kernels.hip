@@ -115,10 +115,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
     scene_tables_to_lds(kp.sc);
     const int lane = threadIdx.x & 63;
-    const Stack stk{stack_mem + threadIdx.x, kBlock, kLdsStack, kp.gstack, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
+    const Stack stk{stack_mem + threadIdx.x, kBlock, kLdsStack,
+                    stack_block(kp.gstack, kp.sc.gdepth, blockIdx.x * kBlock + threadIdx.x), 1u, 0u};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
+    cnt.q[0] = cnt.q[1] = cnt.q[2] = cnt.q[3] = 0;
     const LightStore ls = light_store(kp.lv, kp.fr.lv_max, blockIdx.x * kBlock + threadIdx.x);
     unsigned long long* const work = kp.work;
     const uint64_t total = kp.fr.total_samples;

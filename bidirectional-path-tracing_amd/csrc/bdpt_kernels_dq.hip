@@ -252,6 +252,52 @@ __device__ __forceinline__ float dq_cull_near(const Lane& L) {
     return graze_exempt(L.ray.d, L.h.n, L.h.shape) ? kNoCullNear : kCullNear;
 }
 
+#ifndef BDPT_DQ_AGG
+#define BDPT_DQ_AGG 1  // 1: same-pixel connection contributions of a wave summed in LDS before the framebuffer add
+#endif
+#if BDPT_DQ_AGG
+__shared__ float4 dq_agg[kDqBlock / 64];  // per wave: the running sum of one pixel's contributions
+#endif
+// Adds an eye-side contribution (next-event estimation or a vertex connection)
+// to its pixel. A wave's helpers resolve tasks of a few owners at a time (an
+// owner's 1 + nl tasks share its pixel), so with BDPT_DQ_AGG the lanes adding to
+// one pixel are summed in LDS first and one lane issues the three framebuffer
+// atomics for them (float reassociation only). Called by the lanes that add;
+// the loop runs once per distinct pixel among them.
+__device__ __forceinline__ void dq_add_eye(f3 add, int pixel, float* __restrict__ fb) {
+#if BDPT_DQ_AGG
+    float4& a = dq_agg[threadIdx.x >> 6];
+    bool mine_left = true;
+    for (;;) {
+        const uint64_t pm = __ballot(mine_left);
+        if (!pm) break;
+        const int leader = __ffsll(static_cast<unsigned long long>(pm)) - 1;
+        const int px = __shfl(pixel, leader);
+        const bool mine = mine_left && pixel == px;
+        const bool lead = static_cast<int>(threadIdx.x & 63) == leader;
+        if (lead) a = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (mine) {
+            atomicAdd(&a.x, add.x);
+            atomicAdd(&a.y, add.y);
+            atomicAdd(&a.z, add.z);
+        }
+        if (lead) {
+            const float4 sum = a;
+            float* p = fb + 3 * static_cast<size_t>(px);
+            gadd(p + 0, sum.x);
+            gadd(p + 1, sum.y);
+            gadd(p + 2, sum.z);
+        }
+        mine_left = mine_left && !mine;
+    }
+#else
+    float* p = fb + 3 * static_cast<size_t>(pixel);
+    gadd(p + 0, add.x);
+    gadd(p + 1, add.y);
+    gadd(p + 2, add.z);
+#endif
+}
+
 // The result of the lane's query: owners continue their sample, task lanes add
 // the contribution of an unoccluded shadow ray.
 template <bool COUNT>
@@ -266,11 +312,7 @@ __device__ __forceinline__ uint32_t dq_resolve(Lane& L, int res, float t, float 
                 if (COUNT) cnt.c[6]++;
                 splat_add(fb, L.c.pend_px, L.c.pend);
             } else {
-                const f3 add = L.c.pend * fr.inv_spp;  // rgb[p] += Li * (1 / spp), one connection at a time
-                float* px = fb + 3 * static_cast<size_t>(L.c.pend_px);
-                gadd(px + 0, add.x);
-                gadd(px + 1, add.y);
-                gadd(px + 2, add.z);
+                dq_add_eye(L.c.pend * fr.inv_spp, L.c.pend_px, fb);  // rgb[p] += Li * (1 / spp), per connection
             }
         }
         if (own) {
@@ -561,11 +603,12 @@ __global__ __launch_bounds__(kDqBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel
     scene_tables_to_lds(kp.sc);  // ends with a barrier (the ring's words too)
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
-    const Stack stk{stack_mem + threadIdx.x, kDqBlock, kLdsStack, kp.gstack, kp.nslots,
-                    blockIdx.x * kDqBlock + threadIdx.x};
+    const Stack stk{stack_mem + threadIdx.x, kDqBlock, kLdsStack,
+                    stack_block(kp.gstack, kp.sc.gdepth, blockIdx.x * kDqBlock + threadIdx.x), 1u, 0u};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
+    cnt.q[0] = cnt.q[1] = cnt.q[2] = cnt.q[3] = 0;
     const DqStores st{reinterpret_cast<float4*>(kp.lv), reinterpret_cast<float4*>(kp.ev),
                       static_cast<uint32_t>(kp.fr.lv_max > 1 ? kp.fr.lv_max : 1), kp.ev_max};
     unsigned long long* const work = kp.work;
@@ -603,6 +646,7 @@ __global__ __launch_bounds__(kDqBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel
         asm volatile("" : "+s"(pa));
         const DqParams* P = (const DqParams*)(ConstP)pa;
         // ---- task phase: idle lanes and owners with own tasks get work
+        const uint64_t tp0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
         for (int guard = 0; guard < 64; guard++) {
             const bool own = L.state == ST_BACKLOG;
             const bool idle = L.state == ST_IDLE;
@@ -637,8 +681,10 @@ __global__ __launch_bounds__(kDqBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel
             if (own) got = dq_own_next(L.c, d);
             bool progressed = got;
             if (got) {
+                if (COUNT) cnt.q[own ? 3 : 1]++;
                 if (!own) L.c.prim_tri = static_cast<int>(d);  // (an owner's prim_tri is its primary hit)
                 if (!dq_task<COUNT>(L, d, P->sc, P->fr, st, cnt)) {  // nothing to trace: done at once
+                    if (COUNT) cnt.q[2]++;
                     if (!(d & kDescSelf)) {
                         atomicSub(&cold_u(cold_mem[(d >> 2) & 0xffu].rr), 1u << (16 * ((d >> 10) & 1u)));
                         L.state = ST_IDLE;
@@ -693,6 +739,7 @@ __global__ __launch_bounds__(kDqBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel
             }
             if (!__ballot(progressed)) break;
         }
+        if (COUNT && (threadIdx.x & 63) == 0) cnt.q[0] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - tp0);
         const bool busy = L.state != ST_IDLE;
         if (!__ballot(busy)) {
             // nothing for this wave now: done once no sample is left, the ring is

@@ -820,6 +820,11 @@ __device__ __forceinline__ void flush_counts(const Counts& cnt, unsigned long lo
         for (int off = 32; off > 0; off >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), off)));
         if ((threadIdx.x & 63) == 0 && v) gmax(out + kCounters + i, static_cast<unsigned long long>(v));
     }
+    for (int i = 0; i < 4; i++) {
+        unsigned long long v = cnt.q[i];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((threadIdx.x & 63) == 0 && v) gadd(out + kCounters + 3 + i, v);
+    }
 }
 
 }  // namespace dev

@@ -645,11 +645,12 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
 #endif
     scene_tables_to_lds(P.sc);
     const uint32_t slot = blockIdx.x * 256 + threadIdx.x;
-    const Stack stk{stack_mem + threadIdx.x, 256, kLdsStack, P.gstack, P.nslots, slot};
+    const Stack stk{stack_mem + threadIdx.x, 256, kLdsStack, stack_block(P.gstack, P.sc.gdepth, slot), 1u, 0u};
     const int lane = threadIdx.x & 63;
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
+    cnt.q[0] = cnt.q[1] = cnt.q[2] = cnt.q[3] = 0;
     PtLane L;
     L.busy = false;
     L.q = PQ_NONE;
@@ -764,6 +765,7 @@ __global__ __launch_bounds__(64) void pt_sample_kernel(const PtParams* __restric
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
+    cnt.q[0] = cnt.q[1] = cnt.q[2] = cnt.q[3] = 0;
     // Value-initialised: with a partly uninitialised lane record this one-lane
     // build returned garbage in Li.x (0x5a5a5a5a) although every field is
     // assigned before it is read on the reference's control flow (measured on

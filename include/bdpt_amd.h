@@ -149,6 +149,9 @@ typedef struct {
     int64_t max_queries;     /* ray queries of one sample */
     int64_t schedule_errors; /* lane-decoupled build: connection tasks whose descriptor named no record
                                 (skipped; any non-zero count is a bug, and bdpt_render_host fails) */
+    int64_t sched[4];        /* counting pass of the lane-decoupled build: task-phase wave clocks, tasks
+                                popped from the block rings, tasks that traced no shadow ray, tasks their
+                                owner ran itself (ring full) */
 } bdpt_stats;
 
 const char* bdpt_last_error(void);

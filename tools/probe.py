@@ -37,6 +37,8 @@ out["shade_clock_frac"] = round(c["shade_clocks"] / lc, 4)
 clk = {k: v for k, v in c.items() if k.startswith("clk_")}
 tot = max(sum(clk.values()), 1)
 out["shade_split"] = {k[4:]: round(v / tot, 3) for k, v in clk.items()}
+out["sched_per_sample"] = {k: round(v / n, 3) for k, v in st.get("sched", {}).items()}
+out["kernel"] = st.get("kernel")
 out["kernel_ms"] = round(t_plain, 3)
 out["launches"] = launches
 out["msamples_per_s"] = round(n / t_plain * 1e-3, 3)
