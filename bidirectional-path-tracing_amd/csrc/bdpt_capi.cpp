@@ -66,6 +66,7 @@ hipError_t launch_frame_dq(const dev::DevScene& sc, const dev::DevFrame& fr, flo
                            uint32_t ev_max, uint2* gstack, uint32_t nslots, unsigned long long* work,
                            unsigned long long* counters, int grid, hipStream_t stream, void* dparams);
 int frame_kernel_blocks_per_cu_dq(size_t dyn_lds);
+int frame_kernel_lds_stack_dq();
 size_t pt_params_bytes();
 int pt_blocks_per_cu(size_t dyn_lds);
 hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8], float* fb,
@@ -627,7 +628,9 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     // right children; 4-wide: the host-computed bound), the part beyond the
     // kernel's LDS entries in HBM.
     const int depth = std::max(s->host.max_depth + 2, L.wmax_stack + 1);
-    c->sc.gdepth = static_cast<uint32_t>(std::max(1, depth - frame_kernel_lds_stack()));  // per slot (DevScene::gdepth)
+    // (the builds keep different numbers of entries in LDS: size for the fewest)
+    const int lds_entries = std::min(frame_kernel_lds_stack(), frame_kernel_lds_stack_dq());
+    c->sc.gdepth = static_cast<uint32_t>(std::max(1, depth - lds_entries));  // per slot (DevScene::gdepth)
     const size_t spill_mega = static_cast<size_t>(c->sc.gdepth) * c->nslots;
     HIP_TRY(hipMalloc(&c->gstack, sizeof(uint2) * std::max<size_t>(1, spill_mega)));
     *out = c.release();

@@ -79,16 +79,8 @@ struct DevScene {
     // more than the traversal tree's padding.
     float near_lo[3], near_hi[3];
     uint32_t q_ok;  // qnodes present: the BDPT_QNODES kernels walk the 4-wide tree (else the binary one)
-    // traversal-stack overflow entries per lane slot (the entries past the LDS ones):
-    // slot s's entries are the gstack block [s * gdepth, (s + 1) * gdepth) — one
-    // lane's deep stack touches one page (a subpath trapped in the Caustic glass
-    // sphere walks nested boxes alone for millions of queries)
-    uint32_t gdepth;
+    uint32_t gdepth;  // traversal-stack overflow entries per lane slot (beyond the LDS ones)
 };
-// The overflow block of lane slot `slot` (Stack::gbl with nslots = 1, slot = 0).
-__device__ __forceinline__ uint2* stack_block(uint2* gstack, uint32_t gdepth, uint32_t slot) {
-    return gstack + static_cast<size_t>(slot) * gdepth;
-}
 constexpr uint32_t kNoLds = 0xffffffffu;
 constexpr uint32_t kLdsHdr = 4;  // LDS header words: mt_ring (2 words), mt_ring_stride, unused
 
@@ -532,11 +524,10 @@ __device__ __forceinline__ int shape_id(int packed) { return packed & 0xffffff; 
 #ifndef BDPT_GRAZE
 #define BDPT_GRAZE 1  // 0: the plain |cos| < kGrazeCos test (A/B only; not exact on smooth meshes)
 #endif
-__device__ __forceinline__ bool graze_exempt(f3 d, f3 n, int packed) {
-    const float thr = BDPT_GRAZE ? kGrazeCos + static_cast<float>(static_cast<uint32_t>(packed) >> 24) * 0.015625f
-                                 : kGrazeCos;
-    return fabsf(dot(d, n)) < thr;
+__device__ __forceinline__ float graze_threshold(int packed) {
+    return BDPT_GRAZE ? kGrazeCos + static_cast<float>(static_cast<uint32_t>(packed) >> 24) * 0.015625f : kGrazeCos;
 }
+__device__ __forceinline__ bool graze_exempt(f3 d, f3 n, int packed) { return fabsf(dot(d, n)) < graze_threshold(packed); }
 enum : int { kSlabMiss = 0, kSlabHit = 1, kSlabAmbiguous = 2 };
 struct RayInv {
     f3 inv;

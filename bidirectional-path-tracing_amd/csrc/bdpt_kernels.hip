@@ -66,6 +66,59 @@ constexpr int kBlock = 256;
 #define BDPT_ROOT_LDS 1  // 1: the traversal root and its interior children in LDS, tested when a walk begins (RootLds; measured +1.6 %)
 #endif
 
+#if BDPT_RR == 1 && !BDPT_SAMPLER_STATE
+// Russian roulette: a subpath trapped by total internal reflection bounces
+// between delta surfaces for up to millions of steps, each a
+// closest-hit walk plus the sweep's work for a delta vertex. Once its wave holds
+// nothing else (express mode with one busy lane) those bounces run here, back to
+// back: the walk, then exactly what the sweep does at a delta, non-emitting
+// vertex — the vertex update (bdpt.h:73-136 / :193-209, no connection: delta),
+// ContinuePathRandomWalk (bdpt.h:243-291), the loop test (bdpt.h:68 / :188) —
+// until the chain ends. Out of line: the loop keeps only its own state in
+// registers, where the megakernel's sweep spills (a lone lane waits out every
+// scratch access). Returns true with the result (res, t, u, v) of a query the
+// sweep resolves (a miss, a non-delta or emitting hit); false when the walk
+// ended here (light: ST_DEFER, the eye subpath next; eye: the sample finished).
+__device__ __noinline__ bool express_walk(Lane& Lcaller, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
+                                          const Stack stk, int& res, float& rt, float& ru, float& rv) {
+    Counts cnt;  // (not a counting pass)
+    // the lane's register state as locals (the caller's copy is written back on return)
+    Lane L(Lcaller.c);
+    L.rng = Lcaller.rng, L.state = Lcaller.state, L.ray = Lcaller.ray, L.h = Lcaller.h;
+    struct WriteBack {
+        Lane& to;
+        const Lane& from;
+        __device__ ~WriteBack() { to.rng = from.rng, to.state = from.state, to.ray = from.ray, to.h = from.h; }
+    } wb{Lcaller, L};
+    for (;;) {
+        const bool light = L.state == ST_LIGHT;
+        float t = 0.f, u = 0.f, v = 0.f;
+        const int r = traverse<false, false>(sc, L.ray, false, stk, t, u, v, cnt, cull_near_for(L));
+        const bool hit = r >= 0 && t <= L.ray.max_t && t >= L.ray.min_t;  // accel.h:133
+        const BsdfRecord* b = nullptr;
+        if (hit) b = &bsdf_of(sc, __float_as_int(gld4(sc.shade + kShadeStride * static_cast<size_t>(r)).w));
+        if (!hit || !is_delta(*b) || !is_zero(ld3(b->emission)) || L.c.steps + 1 > (1 << 30)) {
+            res = r, rt = t, ru = u, rv = v;  // the sweep resolves it
+            return true;
+        }
+        ++L.c.steps;  // resolve(): one more query, the hit shaded
+        shade_hit(sc, r, u, v, t, L.ray.d, L.h);
+        const float dist2 = L.h.dist * L.h.dist;
+        BDPT_DIST_TO_GRAZE
+        const float absCosIn = fabsf(L.h.wo.z);
+        L.c.vcm *= div_cr(dist2, absCosIn);
+        L.c.vc *= rcp_cr(absCosIn);
+        L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);  // bdpt.h:129-134 / :201-204
+        const bool more = continue_walk(*b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, L.c.rr);
+        if (!more || !walk_continues(L, fr)) {
+            if (light) L.state = ST_DEFER;  // the eye subpath starts next step
+            else finish<false>(L, fr, fb, cnt);  // L.state = ST_IDLE
+            return false;
+        }
+    }
+}
+#endif
+
 // One query for the lane's pending state, then the state advance.
 template <bool FULL, bool COUNT>
 __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
@@ -115,8 +168,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
     scene_tables_to_lds(kp.sc);
     const int lane = threadIdx.x & 63;
-    const Stack stk{stack_mem + threadIdx.x, kBlock, kLdsStack,
-                    stack_block(kp.gstack, kp.sc.gdepth, blockIdx.x * kBlock + threadIdx.x), 1u, 0u};
+    const Stack stk{stack_mem + threadIdx.x, kBlock, kLdsStack, kp.gstack, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
@@ -239,6 +291,18 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // iterations; a lane whose query finished waits (result kept) until
         // enough lanes of the wave are ready, then those lanes shade together
         // while the slow walkers resume afterwards from where they stopped.
+#if BDPT_RR == 1
+        if (!COUNT && express) {  // a trapped subpath alone in its wave: its delta chain out of line
+            const bool alone = __popcll(__ballot(L.state != ST_IDLE)) == 1;
+            if (alone && !tracing && !has_res && (L.state == ST_LIGHT || L.state == ST_EYE)) {
+                if (express_walk(L, P->sc, P->fr, P->fb, stk, res, rt, ru, rv)) has_res = true;
+                if (!has_res) {
+                    long_walk = false;  // the chain ended: the lane's next step comes from the sweep
+                    continue;
+                }
+            }
+        }
+#endif
         if (L.state != ST_IDLE && !tracing && !has_res) {  // a new query: begin its walk
             q_any = is_shadow_state(L.state);
             if (COUNT && L.state != ST_DEFER) cnt.c[q_any ? 1 : 0]++;

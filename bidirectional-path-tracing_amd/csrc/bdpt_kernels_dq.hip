@@ -25,6 +25,9 @@
 #include <hip/hip_runtime.h>
 
 #define BDPT_BSDF_TABLE 0
+#ifndef BDPT_LDS_STACK
+#define BDPT_LDS_STACK 6  // one traversal-stack entry less in LDS than the default build: room for the task ring
+#endif
 #include "bdpt_path.hpp"
 
 namespace bdpt {
@@ -43,10 +46,13 @@ namespace dev {
 #define BDPT_WALK_UNROLL 1
 #endif
 #ifndef BDPT_DQ_RING
-#define BDPT_DQ_RING 256  // task descriptors per block (LDS)
+#define BDPT_DQ_RING 512  // task descriptors per block (LDS)
 #endif
 #ifndef BDPT_DQ_HELPER_WAVES
 #define BDPT_DQ_HELPER_WAVES 1  // waves per block whose idle lanes take tasks before new samples
+#endif
+#ifndef BDPT_DQ_ROUNDS
+#define BDPT_DQ_ROUNDS 2  // task-phase rounds per loop iteration (a rejected task's lane pops again; 1 / 2 / 64: 152 / 172 / 166)
 #endif
 #ifndef BDPT_DQ_HIGH
 #define BDPT_DQ_HIGH (BDPT_DQ_RING / 2)  // ring fill above which every idle lane takes tasks
@@ -67,7 +73,8 @@ __device__ __forceinline__ uint32_t dq_desc(uint32_t type, uint32_t ol, uint32_t
 // Lane states beyond bdpt_path.hpp's: a task's shadow ray from the camera
 // (connectToCamera) or from an eye vertex; an owner with own tasks still to run;
 // an owner resuming its walk after them.
-enum : uint32_t { ST_TSPLAT = 8, ST_TASK = 9, ST_BACKLOG = 10, ST_RESUME = 11, ST_OTSPLAT = 12, ST_OTASK = 13 };
+enum : uint32_t { ST_TSPLAT = 8, ST_TASK = 9, ST_BACKLOG = 10, ST_RESUME = 11, ST_OTSPLAT = 12, ST_OTASK = 13,
+                  ST_FINWAIT = 14 };
 // ST_OTSPLAT / ST_OTASK: an owner's own task (its descriptor is not kept: the
 // owner's LaneCold still holds its sample, prim_tri included)
 enum : uint32_t { A_PUSH = 20, A_RESUME_LIGHT, A_RESUME_EYE };
@@ -252,51 +259,18 @@ __device__ __forceinline__ float dq_cull_near(const Lane& L) {
     return graze_exempt(L.ray.d, L.h.n, L.h.shape) ? kNoCullNear : kCullNear;
 }
 
-#ifndef BDPT_DQ_AGG
-#define BDPT_DQ_AGG 1  // 1: same-pixel connection contributions of a wave summed in LDS before the framebuffer add
-#endif
-#if BDPT_DQ_AGG
-__shared__ float4 dq_agg[kDqBlock / 64];  // per wave: the running sum of one pixel's contributions
-#endif
-// Adds an eye-side contribution (next-event estimation or a vertex connection)
-// to its pixel. A wave's helpers resolve tasks of a few owners at a time (an
-// owner's 1 + nl tasks share its pixel), so with BDPT_DQ_AGG the lanes adding to
-// one pixel are summed in LDS first and one lane issues the three framebuffer
-// atomics for them (float reassociation only). Called by the lanes that add;
-// the loop runs once per distinct pixel among them.
-__device__ __forceinline__ void dq_add_eye(f3 add, int pixel, float* __restrict__ fb) {
-#if BDPT_DQ_AGG
-    float4& a = dq_agg[threadIdx.x >> 6];
-    bool mine_left = true;
-    for (;;) {
-        const uint64_t pm = __ballot(mine_left);
-        if (!pm) break;
-        const int leader = __ffsll(static_cast<unsigned long long>(pm)) - 1;
-        const int px = __shfl(pixel, leader);
-        const bool mine = mine_left && pixel == px;
-        const bool lead = static_cast<int>(threadIdx.x & 63) == leader;
-        if (lead) a = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (mine) {
-            atomicAdd(&a.x, add.x);
-            atomicAdd(&a.y, add.y);
-            atomicAdd(&a.z, add.z);
-        }
-        if (lead) {
-            const float4 sum = a;
-            float* p = fb + 3 * static_cast<size_t>(px);
-            gadd(p + 0, sum.x);
-            gadd(p + 1, sum.y);
-            gadd(p + 2, sum.z);
-        }
-        mine_left = mine_left && !mine;
-    }
-#else
-    float* p = fb + 3 * static_cast<size_t>(pixel);
-    gadd(p + 0, add.x);
-    gadd(p + 1, add.y);
-    gadd(p + 2, add.z);
-#endif
+// Eye-side contributions (next-event estimation, vertex connections) go to the
+// owner's eye estimate in LDS (LaneCold::Li, three ds_add_f32), as the serial
+// schedule adds them to its Li: the owner adds the estimate to the framebuffer
+// once, when its sample has ended AND every task of it is done (ST_FINWAIT
+// until then; the lane takes ring tasks meanwhile). The sums differ from the
+// reference's only in order (float reassociation, like the atomics).
+__device__ __forceinline__ void dq_li_add(LaneCold& owner, f3 v) {
+    atomicAdd(&owner.Li.x, v.x);
+    atomicAdd(&owner.Li.y, v.y);
+    atomicAdd(&owner.Li.z, v.z);
 }
+constexpr uint32_t kFinWait = 1u << 16;  // LaneCold::nl: the owner's sample ended, its tasks are not all done
 
 // The result of the lane's query: owners continue their sample, task lanes add
 // the contribution of an unoccluded shadow ray.
@@ -312,7 +286,8 @@ __device__ __forceinline__ uint32_t dq_resolve(Lane& L, int res, float t, float 
                 if (COUNT) cnt.c[6]++;
                 splat_add(fb, L.c.pend_px, L.c.pend);
             } else {
-                dq_add_eye(L.c.pend * fr.inv_spp, L.c.pend_px, fb);  // rgb[p] += Li * (1 / spp), per connection
+                // Li += contribution of the owner's sample (bdpt.h:140, :150)
+                dq_li_add(own ? L.c : cold[(static_cast<uint32_t>(L.c.prim_tri) >> 2) & 0xffu], L.c.pend);
             }
         }
         if (own) {
@@ -321,8 +296,8 @@ __device__ __forceinline__ uint32_t dq_resolve(Lane& L, int res, float t, float 
         }
         const uint32_t d = static_cast<uint32_t>(L.c.prim_tri);
         const uint32_t ol = (d >> 2) & 0xffu, buf = (d >> 10) & 1u;
-        atomicSub(&cold_u(cold[ol].rr), 1u << (16 * buf));
-        L.state = ST_IDLE;
+        atomicSub(&cold_u(cold[ol].rr), 1u << (16 * buf));  // after the Li add (LDS is in order per wave)
+        L.state = (static_cast<uint32_t>(L.c.nl) & kFinWait) ? ST_FINWAIT : ST_IDLE;
         return A_DONE;
     }
     bool hit = res >= 0 && t <= L.ray.max_t && t >= L.ray.min_t;  // accel.h:133
@@ -407,14 +382,15 @@ __device__ void dq_advance(Lane& L, uint32_t act, const DevScene& sc, const DevF
                     const float pA = rcp_cr(e.area * emitterPdf);
                     const float camW = pA * L.c.vcm + (pA * kInvTwoPi) * L.c.vc;
                     const float mis = rcp_cr(1.f + camW);
+                    // (Li in LDS takes helpers' adds concurrently: atomic adds)
                     if (fr.strategy == 2) {
-                        if (L.c.pure) L.c.Li = L.c.Li + contrib;
+                        if (L.c.pure) dq_li_add(L.c, contrib);
                     } else {
                         if (!L.c.pure) contrib = contrib * mis;
-                        L.c.Li = L.c.Li + contrib;
+                        dq_li_add(L.c, contrib);
                     }
                 } else if (L.c.depth == 1) {
-                    L.c.Li = L.c.Li + emission;
+                    dq_li_add(L.c, emission);
                 }
             }
             act = A_FINISH;
@@ -568,11 +544,10 @@ __device__ void dq_advance(Lane& L, uint32_t act, const DevScene& sc, const DevF
             act = A_FINISH;
         }
     } DQ_END;
-    DQ_ACTION(31, act == A_FINISH) {
-        finish<COUNT>(L, fr, fb, cnt);  // the sample's own eye estimate (emitter hits); L.state = ST_IDLE
-        const uint64_t m = __ballot(true);
-        if ((threadIdx.x & 63) == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(m)) - 1))
-            atomicSub(&q.owners, static_cast<uint32_t>(__popcll(m)));
+    DQ_ACTION(31, act == A_FINISH) {  // the sample's walks have ended: its estimate once its tasks are done
+        L.c.nl = static_cast<int>(static_cast<uint32_t>(L.c.nl) | kFinWait);
+        L.state = ST_FINWAIT;
+        act = A_ISSUED;
     } DQ_END;
 }
 #undef DQ_ACTION
@@ -603,8 +578,8 @@ __global__ __launch_bounds__(kDqBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel
     scene_tables_to_lds(kp.sc);  // ends with a barrier (the ring's words too)
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
-    const Stack stk{stack_mem + threadIdx.x, kDqBlock, kLdsStack,
-                    stack_block(kp.gstack, kp.sc.gdepth, blockIdx.x * kDqBlock + threadIdx.x), 1u, 0u};
+    const Stack stk{stack_mem + threadIdx.x, kDqBlock, kLdsStack, kp.gstack, kp.nslots,
+                    blockIdx.x * kDqBlock + threadIdx.x};
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
@@ -647,15 +622,28 @@ __global__ __launch_bounds__(kDqBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel
         const DqParams* P = (const DqParams*)(ConstP)pa;
         // ---- task phase: idle lanes and owners with own tasks get work
         const uint64_t tp0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
-        for (int guard = 0; guard < 64; guard++) {
-            const bool own = L.state == ST_BACKLOG;
-            const bool idle = L.state == ST_IDLE;
-            if (!__ballot(own || idle)) break;
-            const uint32_t buf_next = dq_buf(L.c) ^ 1u;
+        for (int round = 0; round < BDPT_DQ_ROUNDS; round++) {
             const uint32_t pend = __hip_atomic_load(&cold_u(L.c.rr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            {  // owners whose sample ended: its estimate to the framebuffer once its last task is done
+                const bool fin = L.state == ST_FINWAIT && ((pend >> (16 * dq_buf(L.c))) & 0xffffu) == 0u;
+                const uint64_t fm = __ballot(fin);
+                if (fm) {
+                    if (fin) {
+                        L.c.nl = static_cast<int>(static_cast<uint32_t>(L.c.nl) & ~kFinWait);
+                        finish<COUNT>(L, P->fr, P->fb, cnt);  // L.state = ST_IDLE
+                    }
+                    if (lane == __ffsll(static_cast<unsigned long long>(fm)) - 1)
+                        atomicSub(&q.owners, static_cast<uint32_t>(__popcll(fm)));
+                }
+            }
+            const bool own = L.state == ST_BACKLOG;
+            const bool waiting = L.state == ST_FINWAIT;  // (may help meanwhile)
+            const bool idle = L.state == ST_IDLE;
+            if (!__ballot(own || idle || waiting)) break;
+            const uint32_t buf_next = dq_buf(L.c) ^ 1u;
             const bool can_sample = idle && !exhausted && ((pend >> (16 * buf_next)) & 0xffffu) == 0u;
             const uint32_t fill = dq_load(q.tail) - dq_load(q.head);  // snapshot (policy only)
-            const bool want = idle && fill > 0u && (fill > take_at || !can_sample);
+            const bool want = (idle && fill > 0u && (fill > take_at || !can_sample)) || (waiting && fill > 0u);
             uint32_t d = 0;
             bool got = false;
             const uint64_t wm = __ballot(want);
@@ -687,7 +675,7 @@ __global__ __launch_bounds__(kDqBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel
                     if (COUNT) cnt.q[2]++;
                     if (!(d & kDescSelf)) {
                         atomicSub(&cold_u(cold_mem[(d >> 2) & 0xffu].rr), 1u << (16 * ((d >> 10) & 1u)));
-                        L.state = ST_IDLE;
+                        L.state = waiting ? ST_FINWAIT : ST_IDLE;
                     }
                 }
             } else if (own) {  // backlog done: the walk resumes in the next shading step
@@ -750,7 +738,7 @@ __global__ __launch_bounds__(kDqBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel
         }
         // ---- walk (the overlapped schedule of bdpt_kernels.hip)
         // (an owner still in ST_BACKLOG, when the task phase ran out of rounds, waits for the next one)
-        if (busy && !tracing && !has_res && L.state != ST_BACKLOG) {
+        if (busy && !tracing && !has_res && L.state != ST_BACKLOG && L.state != ST_FINWAIT) {
             q_any = dq_is_shadow(L.state);
             if (COUNT && L.state != ST_DEFER && L.state != ST_RESUME) cnt.c[q_any ? 1 : 0]++;
             ri = ray_inv(L.ray, dq_cull_near(L));
@@ -774,6 +762,10 @@ __global__ __launch_bounds__(kDqBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel
                     has_res = true;
                 }
             }
+        }
+        if (!__ballot(tracing || has_res)) {  // only owners waiting on their tasks (or own tasks next round)
+            __builtin_amdgcn_s_sleep(1);
+            continue;
         }
         const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
         for (;;) {
@@ -843,6 +835,8 @@ hipError_t launch_frame_dq(const dev::DevScene& sc, const dev::DevFrame& fr, flo
     else hipLaunchKernelGGL((dev::bdpt_frame_kernel_dq<false, false, false>), g, b, lds, stream, kp);
     return hipGetLastError();
 }
+
+int frame_kernel_lds_stack_dq() { return dev::kLdsStack; }
 
 int frame_kernel_blocks_per_cu_dq(size_t dyn_lds) {
     int n = 0;

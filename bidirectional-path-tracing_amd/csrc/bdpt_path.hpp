@@ -388,6 +388,17 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
     return true;
 }
 
+// BDPT_GRAZE_IN_DIST 1: a vertex's near-cull threshold (graze_threshold) is
+// decoded once, in its vertex body, into Hit::dist (dead after that body), and
+// the queries leaving the vertex compare against it (cull_near_for).
+#ifndef BDPT_GRAZE_IN_DIST
+#define BDPT_GRAZE_IN_DIST 0
+#endif
+#if BDPT_GRAZE_IN_DIST
+#define BDPT_DIST_TO_GRAZE L.h.dist = graze_threshold(L.h.shape);
+#else
+#define BDPT_DIST_TO_GRAZE
+#endif
 #ifndef BDPT_SPLIT_CONTINUE
 #define BDPT_SPLIT_CONTINUE 0  // 1: the light subpath's continuation runs before the eye subpath's start, so a light walk that ends starts its eye walk in the same sweep (no ST_DEFER step); the eye continuation is its own body
 #endif
@@ -395,6 +406,7 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
 #define BDPT_BODY_LIGHT_VERTEX \
     BDPT_ACTION(26, act == A_LIGHT_VERTEX) {  /* bdpt.h:193-209 */ \
         const float dist2 = L.h.dist * L.h.dist; \
+        BDPT_DIST_TO_GRAZE \
         const float absCosIn = fabsf(L.h.wo.z); \
         L.c.vcm *= div_cr(dist2, absCosIn); \
         L.c.vc *= rcp_cr(absCosIn); \
@@ -525,6 +537,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
     } BDPT_END;
     BDPT_ACTION(22, act == A_EYE_VERTEX) {  // bdpt.h:73-136
         const float dist2 = L.h.dist * L.h.dist;
+        BDPT_DIST_TO_GRAZE
         const float absCosIn = fabsf(L.h.wo.z);
         L.c.vcm *= div_cr(dist2, absCosIn);
         L.c.vc *= rcp_cr(absCosIn);
@@ -585,6 +598,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
 #define BDPT_EMIT_GRAZE 1  // 0: the emitter face's graze code is not used (A/B only)
 #endif
         if (BDPT_EMIT_GRAZE) L.h.shape = e_graze;  // its graze code (the shape id is not read before the walk's resolve)
+        if (BDPT_GRAZE_IN_DIST) L.h.dist = graze_threshold(e_graze);
         L.c.tp = (ld3(e.radiance) * edir.z) * rcp_cr(emissionPdf);
         L.c.vc = edir.z * rcp_cr(emissionPdf);
         L.c.vcm = div_cr(areaPdf, emissionPdf);
@@ -749,7 +763,11 @@ __device__ __forceinline__ bool is_shadow_state(uint32_t st) { return st == ST_S
 __device__ __forceinline__ float cull_near_for(const Lane& L) {
     const uint32_t st = L.state;
     if (st == ST_PRIMARY || st == ST_SPLAT) return kCullNear;
+#if BDPT_GRAZE_IN_DIST
+    return fabsf(dot(L.ray.d, L.h.n)) < L.h.dist ? kNoCullNear : kCullNear;
+#else
     return graze_exempt(L.ray.d, L.h.n, L.h.shape) ? kNoCullNear : kCullNear;
+#endif
 }
 
 // Applies the result of the lane's pending query (closest hit: leaf-order

@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kKatBlock) void intersect_kat_kernel(DevScene sc, i
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kKatBlock + threadIdx.x;
     if (i >= n) return;
     const uint32_t slot = static_cast<uint32_t>(i % nslots);
-    const Stack stk{stack_mem + threadIdx.x, kKatBlock, kLdsStack, stack_block(gstack, sc.gdepth, slot), 1u, 0u};
+    const Stack stk{stack_mem + threadIdx.x, kKatBlock, kLdsStack, gstack, nslots, slot};
     const float* r = rays + 8 * i;
     const Ray ray{mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], r[7]};
     Counts cnt;

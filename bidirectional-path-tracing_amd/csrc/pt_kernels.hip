@@ -645,7 +645,7 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
 #endif
     scene_tables_to_lds(P.sc);
     const uint32_t slot = blockIdx.x * 256 + threadIdx.x;
-    const Stack stk{stack_mem + threadIdx.x, 256, kLdsStack, stack_block(P.gstack, P.sc.gdepth, slot), 1u, 0u};
+    const Stack stk{stack_mem + threadIdx.x, 256, kLdsStack, P.gstack, P.nslots, slot};
     const int lane = threadIdx.x & 63;
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;

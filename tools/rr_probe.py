@@ -15,6 +15,20 @@ import torch  # noqa: E402
 import bdpt_amd  # noqa: E402
 import variants  # noqa: E402
 
+def _beat():  # a line every 30 s: one Russian-roulette frame can run for minutes
+    import threading
+
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(30)
+            print(f"[rr_probe] running, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
+_beat()
 a = sys.argv[1:]
 name = a[0] if a else "caustic"
 W, H, spp = (int(x) for x in (a[1:4] if len(a) >= 4 else (512, 512, 4)))
@@ -24,7 +38,8 @@ cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**sc["camera"]), width=W, height=H,
                       russian_roulette=bdpt_amd.RR_LUMINANCE)
 it = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(name)), cfg)
 it.init()
-for flags, label in ((0, "render"), (bdpt_amd.FLAG_COUNT, "counting")):
+passes = ((0, "render"),) if os.environ.get("RR_PROBE_NO_COUNT") else ((0, "render"), (bdpt_amd.FLAG_COUNT, "counting"))
+for flags, label in passes:
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
     t = time.time()
@@ -37,5 +52,5 @@ for flags, label in ((0, "render"), (bdpt_amd.FLAG_COUNT, "counting")):
            "kernel": st["kernel"]}
     if flags:
         out.update(max_light_depth=st["max_light_depth"], max_eye_depth=st["max_eye_depth"],
-                   max_queries=st["max_queries"])
+                   max_queries=st["max_queries"], counters=st["counters"])
     print(json.dumps(out), flush=True)
