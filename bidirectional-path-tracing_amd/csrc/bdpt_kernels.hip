@@ -66,7 +66,10 @@ constexpr int kBlock = 256;
 #define BDPT_ROOT_LDS 1  // 1: the traversal root and its interior children in LDS, tested when a walk begins (RootLds; measured +1.6 %)
 #endif
 
-#if BDPT_RR == 1 && !BDPT_SAMPLER_STATE
+#ifndef BDPT_EXPRESS_WALK
+#define BDPT_EXPRESS_WALK 0  // 1: a lone trapped lane's delta chain out of line (express_walk; 1.5 % faster on the trapped chain, +49 VGPR spills in the RR build)
+#endif
+#if BDPT_RR == 1 && !BDPT_SAMPLER_STATE && BDPT_EXPRESS_WALK
 // Russian roulette: a subpath trapped by total internal reflection bounces
 // between delta surfaces for up to millions of steps, each a
 // closest-hit walk plus the sweep's work for a delta vertex. Once its wave holds
@@ -157,6 +160,19 @@ struct KParams {
 // SLACK: interior boxes with slab_fast's ambiguity slack (DevScene::node_slack,
 // decided per render on the host); a template parameter so the node step of
 // the walk loop carries no branch on it.
+#ifndef BDPT_TAIL_CHUNK
+#define BDPT_TAIL_CHUNK 4  // x the grid's lanes from the end: finer claims (0: 64-sample chunks throughout)
+#endif
+#ifndef BDPT_CLAIM_SCALAR
+#define BDPT_CLAIM_SCALAR 1  // the claimed chunk base broadcast by readfirstlane (scalar) instead of a shuffle
+#endif
+// Samples the wave claims next, from the last chunk it claimed (wave-uniform).
+__device__ __forceinline__ uint64_t tail_chunk(uint64_t last_base, uint64_t total) {
+    if (!BDPT_TAIL_CHUNK) return 64;
+    const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * kBlock;
+    return last_base + BDPT_TAIL_CHUNK * lanes < total ? 64 : last_base + lanes / 2 < total ? 16 : 4;
+}
+
 template <bool FULL, bool COUNT, bool SLACK>
 __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(const KParams* __restrict__ kpp) {
     const KParams& kp = *kpp;
@@ -222,7 +238,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         uint64_t pa = (uint64_t)(ConstKParams)kpp;
         asm volatile("" : "+s"(pa));
         const KParams* P = (const KParams*)(ConstKParams)pa;
-        const bool express = BDPT_RR == 1 && __ballot(long_walk) != 0;  // wave-uniform
+        const bool express = BDPT_RR == 1 && BDPT_EXPRESS_DEPTH > 0 && __ballot(long_walk) != 0;  // wave-uniform
 #if BDPT_SEED_CHUNK
         // Refill idle lanes from the wave's chunk of 64 consecutive samples. A
         // chunk is claimed with one atomic and the seeding recurrence of all its
@@ -236,17 +252,30 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     exhausted = true;
                     break;
                 }
+                // Near the frame's end a wave's unstarted chunk samples wait for
+                // its busy lanes (up to a whole sample's latency) while other
+                // waves run dry: once the claims seen by this wave come within
+                // BDPT_TAIL_CHUNK x the grid's lanes of the end, claim 16, then
+                // 4 samples at a time (any sizes partition [0, total)).
+                const uint64_t want = tail_chunk(chunk_base, total);
                 unsigned long long base = 0;
-                if (lane == 0) base = gadd(work, 64ull);
+                if (lane == 0) base = gadd(work, static_cast<unsigned long long>(want));
+#if BDPT_CLAIM_SCALAR
+                // wave-uniform in scalar registers (a shuffle's result is a VGPR pair)
+                base = static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base))) |
+                       static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base >> 32)))
+                           << 32;
+#else
                 base = __shfl(base, 0);
+#endif
                 if (base >= total) {
                     exhausted = true;
                     break;
                 }
                 chunk_base = base;
-                chunk_n = static_cast<int>(total - base < 64 ? total - base : 64);
+                chunk_n = static_cast<int>(total - base < want ? total - base : want);
                 chunk_pos = 0;
-                global_done = base + 64 >= total;
+                global_done = base + want >= total;
                 if (BDPT_DIAG && global_done && lane == 0 && P->fr.diag)  // the frame's last chunk (one wave claims it)
                     P->fr.diag[kDiagLastClaim] = __builtin_amdgcn_s_memrealtime();
                 int px;
@@ -291,7 +320,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // iterations; a lane whose query finished waits (result kept) until
         // enough lanes of the wave are ready, then those lanes shade together
         // while the slow walkers resume afterwards from where they stopped.
-#if BDPT_RR == 1
+#if BDPT_RR == 1 && BDPT_EXPRESS_WALK
         if (!COUNT && express) {  // a trapped subpath alone in its wave: its delta chain out of line
             const bool alone = __popcll(__ballot(L.state != ST_IDLE)) == 1;
             if (alone && !tracing && !has_res && (L.state == ST_LIGHT || L.state == ST_EYE)) {
