@@ -739,9 +739,9 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     dev::DevScene sc = c->sc;
     sc.node_slack = node_slack_needed(c, eye, 1);
     if (p->rr_depth > kLazyRrDepth || rr) {  // draws past 226: the lanes' MT19937 rings
-        if (!c->mt_ring) HIP_TRY(hipMalloc(&c->mt_ring, sizeof(uint32_t) * 624 * static_cast<size_t>(c->nslots)));
+        if (!c->mt_ring) HIP_TRY(hipMalloc(&c->mt_ring, sizeof(uint32_t) * kMtRingSlotWords * static_cast<size_t>(c->nslots)));
         sc.mt_ring = c->mt_ring;
-        sc.mt_ring_stride = 1;  // slot-major blocks of 624 words (DevScene::mt_ring)
+        sc.mt_ring_stride = 1;  // slot-major blocks of kMtRingSlotWords words (DevScene::mt_ring)
     }
     if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
@@ -1163,8 +1163,9 @@ int bdpt_render_host(bdpt_ctx* c, const bdpt_frame_params* p, float* fb_host) {
         bdpt_stats st;
         if ((rc = bdpt_get_stats(c, &st))) return rc;
         if (st.schedule_errors)
-            return fail(BDPT_ERR_HIP, std::to_string(st.schedule_errors) + " connection tasks named no record "
-                                                                           "(lane-decoupled build)");
+            return fail(BDPT_ERR_HIP, std::to_string(st.schedule_errors) +
+                                          " schedule errors (a lane-decoupled connection task that named no record, "
+                                          "or MT19937 draws past the generated ring)");
         if (p->russian_roulette && st.capped_samples)
             return fail(BDPT_ERR_UNSUPPORTED, std::to_string(st.capped_samples) +
                                                   " samples met the Russian-roulette bounds (light-vertex store / "

@@ -66,7 +66,7 @@ struct DevScene {
     uint32_t lds_etri_off, lds_ecdf_off;
     int32_t n_etri, n_ecdf;
     // MT19937 continuation ring of the megakernel's lanes (rrDepth > 28, Russian
-    // roulette): word k of lane slot s at mt_ring[s * 624 + k] (one 2.5 KB block per
+    // roulette): word k of lane slot s at mt_ring[s * kMtRingSlotWords + k] (one 2.5 KB block per
     // slot: a lane's draws touch one page, not 624 pages a slot-count stride apart —
     // a Russian-roulette subpath trapped in glass draws millions of them alone);
     // mt_ring_stride is the word stride within a block (1); null otherwise
@@ -332,16 +332,83 @@ __device__ __forceinline__ uint32_t mt_seed_from(uint32_t x, uint32_t i) {
 // host refuses such depths elsewhere). The ring of this lane slot is found
 // through the LDS header. Only this build carries the branch and the call at
 // every draw site: in the default build they cost ~30 % of the throughput.
+#ifndef BDPT_RING_AHEAD
+#define BDPT_RING_AHEAD 32  // draws generated ahead into the ring at one call site per shading step (0: per draw)
+#endif
+#if BDPT_RING_AHEAD
+// The ring, generated ahead: outputs n >= 227 are produced by mt_ring_ahead,
+// called once per shading step (before the sweep) for lanes within
+// BDPT_RING_AHEAD draws of the ring, so every draw site reads
+// ring[n mod 624] (one load, no call: an out-of-line call at each of the ~20
+// draw sites made the caller keep its live registers in scratch). A sweep draws
+// far fewer than BDPT_RING_AHEAD numbers (the action DAG's draw sites sum to
+// < 20). Per lane slot kMtRingWords words: the 624-word ring, then the
+// generator's cursor (x[g], x[g+1] of the seeding sequence while g < 623, g,
+// the seed whose outputs the ring holds).
+constexpr uint32_t kMtRingWords = kMtRingSlotWords;
+__device__ __forceinline__ uint32_t* mt_ring_slot() {
+    const uint64_t base = (static_cast<uint64_t>(g_scene_lds[1]) << 32) | g_scene_lds[0];
+    return reinterpret_cast<uint32_t*>(base) + static_cast<size_t>(blockIdx.x * blockDim.x + threadIdx.x) * kMtRingWords;
+}
+// Generates outputs up to r.n + BDPT_RING_AHEAD - 1; false if the lane had
+// already drawn past what was generated (a schedule error: the caller reports it).
+__device__ BDPT_NOINLINE bool mt_ring_ahead(const LazyMT& r) {
+    uint32_t* const ring = mt_ring_slot();
+    uint32_t xa0 = ring[624], xa1 = ring[625], g = ring[626];
+    const uint32_t want = r.n + BDPT_RING_AHEAD;
+    if (r.n < 227) {  // (x[n], x[n+1], x[n+397]) still in registers: the seed is recoverable
+        const uint32_t seed = mt_seed_from(r.a0, r.n);
+        // another seed's outputs, or this seed's past the window that still holds
+        // output 227 (g > 851): outputs 0..226 again
+        if (ring[627] != seed || g < 227 || g > 851) {
+            uint32_t a0 = seed, a1 = mt_init_step(seed, 1), b = seed;
+            for (uint32_t i = 1; i <= 397; i++) b = mt_init_step(b, i);
+            for (uint32_t k = 0; k < 227; k++) {
+                ring[k] = mt_twist(a0, a1, b);
+                a0 = a1;
+                a1 = mt_init_step(a1, k + 2);
+                b = mt_init_step(b, k + 398);
+            }
+            xa0 = a0, xa1 = a1, g = 227;  // x[227], x[228]
+            ring[627] = seed;
+        }
+    } else if (g < r.n) {
+        return false;
+    }
+    if (g >= want) return true;
+    for (; g < want; g++) {
+        uint32_t un, un1;
+        if (g < 623) un = xa0, un1 = xa1;
+        else if (g == 623) un = xa0, un1 = ring[0];
+        else un = ring[(g - 624) % 624], un1 = ring[(g - 623) % 624];
+        ring[g % 624] = mt_twist(un, un1, ring[(g - 227) % 624]);
+        if (g + 2 <= 623) {
+            xa0 = xa1;
+            xa1 = mt_init_step(xa1, g + 2);
+        } else if (g + 1 <= 623) {
+            xa0 = xa1;
+        }
+    }
+    ring[624] = xa0, ring[625] = xa1, ring[626] = g;
+    return true;
+}
+__device__ __forceinline__ uint32_t mt_u32_long(LazyMT& r) {
+    const uint32_t v = mt_ring_slot()[r.n % 624];
+    r.n++;
+    return mt_temper(v);
+}
+#else
+constexpr uint32_t kMtRingWords = 624;
 __device__ BDPT_NOINLINE uint32_t mt_u32_long(LazyMT& r) {
     const uint64_t base = (static_cast<uint64_t>(g_scene_lds[1]) << 32) | g_scene_lds[0];
     uint32_t* const ring = reinterpret_cast<uint32_t*>(base);
     if (!ring) return mt_next_u32(r);  // unreachable (host check)
     const uint32_t st = g_scene_lds[2];
     const uint32_t seed = r.n == 227 ? mt_seed_from(r.a0, 227) : 0u;
-    return mt_ring_step(r, seed, ring + static_cast<size_t>(blockIdx.x * blockDim.x + threadIdx.x) * 624, st);
+    return mt_ring_step(r, seed, ring + static_cast<size_t>(blockIdx.x * blockDim.x + threadIdx.x) * kMtRingWords, st);
 }
-
-#endif
+#endif  // BDPT_RING_AHEAD
+#endif  // BDPT_DEEP_RNG
 
 // generate_canonical<float, 24> (libstdc++ 11 random.tcc:3348-3380).
 __device__ __forceinline__ float next1(LazyMT& r) {
@@ -661,20 +728,33 @@ typedef u32x2 gbl_uint2;
 typedef uint32_t lds_u32;
 typedef uint32_t gbl_u32;
 #endif
+// threadIdx.x, re-read at each use (opaque to the optimiser): per-lane
+// addresses derived from it at their use are not held in registers across the
+// persistent loop (only threadIdx.x itself is).
+__device__ __forceinline__ uint32_t opaque_tid() {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 struct Stack {
     uint2* lds;
     int stride;
     int nlds;    // entries held in LDS
     uint2* gbl;  // entry k >= nlds at gbl[(k - nlds) * nslots + slot] (the frame kernels: the slot's block, nslots 1)
     uint32_t nslots, slot;
+    bool tid_rel = false;  // lds and slot are the block's bases; the lane adds threadIdx.x at each access
+    __device__ __forceinline__ uint32_t lane_off() const { return tid_rel ? opaque_tid() : 0u; }
     __device__ __forceinline__ void put(int k, uint32_t link, float tn) const {
         const u32x2 e = {link, __float_as_uint(tn)};
-        if (k < nlds) ((lds_uint2*)lds)[k * stride] = e;
-        else ((gbl_uint2*)gbl)[static_cast<size_t>(k - nlds) * nslots + slot] = e;
+        const uint32_t t = lane_off();
+        if (k < nlds) ((lds_uint2*)lds)[t + k * stride] = e;
+        else ((gbl_uint2*)gbl)[static_cast<size_t>(k - nlds) * nslots + slot + t] = e;
     }
     __device__ __forceinline__ uint2 get(int k) const {
-        const u32x2 e = k < nlds ? ((const lds_uint2*)lds)[k * stride]
-                                 : ((const gbl_uint2*)gbl)[static_cast<size_t>(k - nlds) * nslots + slot];
+        const uint32_t t = lane_off();
+        const u32x2 e = k < nlds ? ((const lds_uint2*)lds)[t + k * stride]
+                                 : ((const gbl_uint2*)gbl)[static_cast<size_t>(k - nlds) * nslots + slot + t];
         return make_uint2(e.x, e.y);
     }
 };

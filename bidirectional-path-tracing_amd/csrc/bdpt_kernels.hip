@@ -109,6 +109,9 @@ __device__ __noinline__ bool express_walk(Lane& Lcaller, const DevScene& sc, con
         const float dist2 = L.h.dist * L.h.dist;
         BDPT_DIST_TO_GRAZE
         const float absCosIn = fabsf(L.h.wo.z);
+#if BDPT_RING_AHEAD
+        if (L.rng.n + BDPT_RING_AHEAD >= 227 && !mt_ring_ahead(L.rng) && fr.diag) gadd(fr.diag + kDiagErrors, 1ull);
+#endif
         L.c.vcm *= div_cr(dist2, absCosIn);
         L.c.vc *= rcp_cr(absCosIn);
         L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);  // bdpt.h:129-134 / :201-204
@@ -132,6 +135,9 @@ __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame
     const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     const int res = query ? traverse<FULL, COUNT>(sc, L.ray, any, stk, t, u, v, cnt, cull_near_for(L)) : -1;
     const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+#if BDPT_DEEP_RNG && BDPT_RING_AHEAD
+    if (L.rng.n + BDPT_RING_AHEAD >= 227 && !mt_ring_ahead(L.rng) && fr.diag) gadd(fr.diag + kDiagErrors, 1ull);
+#endif
     const uint32_t act = resolve<COUNT>(L, res, t, u, v, sc, fr, fb, cnt);
     advance<COUNT>(L, act, sc, fr, fb, ls, cnt);
     if (COUNT && first_active_lane()) {  // wave clocks in traversal / in the state advance
@@ -160,6 +166,9 @@ struct KParams {
 // SLACK: interior boxes with slab_fast's ambiguity slack (DevScene::node_slack,
 // decided per render on the host); a template parameter so the node step of
 // the walk loop carries no branch on it.
+#ifndef BDPT_TID_REMAT
+#define BDPT_TID_REMAT 1  // the lane's traversal-stack and light-vertex addresses re-derived from threadIdx.x at each use
+#endif
 #ifndef BDPT_TAIL_CHUNK
 #define BDPT_TAIL_CHUNK 4  // x the grid's lanes from the end: finer claims (0: 64-sample chunks throughout)
 #endif
@@ -184,12 +193,21 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
     scene_tables_to_lds(kp.sc);
     const int lane = threadIdx.x & 63;
+#if BDPT_TID_REMAT
+    const Stack stk{stack_mem, kBlock, kLdsStack, kp.gstack, kp.nslots, blockIdx.x * kBlock, true};
+#else
     const Stack stk{stack_mem + threadIdx.x, kBlock, kLdsStack, kp.gstack, kp.nslots, blockIdx.x * kBlock + threadIdx.x};
+#endif
     Counts cnt;
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
     cnt.q[0] = cnt.q[1] = cnt.q[2] = cnt.q[3] = 0;
+#if BDPT_TID_REMAT
+    LightStore ls = light_store(kp.lv, kp.fr.lv_max, blockIdx.x * kBlock);
+    ls.tid_rel = true;
+#else
     const LightStore ls = light_store(kp.lv, kp.fr.lv_max, blockIdx.x * kBlock + threadIdx.x);
+#endif
     unsigned long long* const work = kp.work;
     const uint64_t total = kp.fr.total_samples;
     __shared__ LaneCold cold_mem[kBlock];
@@ -394,6 +412,11 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
         if (has_res) {
             has_res = false;
+#if BDPT_DEEP_RNG && BDPT_RING_AHEAD
+            // the draws of this step past 227 are read from the ring: generate them first
+            if (L.rng.n + BDPT_RING_AHEAD >= 227 && !mt_ring_ahead(L.rng) && P->fr.diag)
+                gadd(P->fr.diag + kDiagErrors, 1ull);
+#endif
             const uint64_t r0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
             const uint32_t act = resolve<COUNT>(L, res, rt, ru, rv, P->sc, P->fr, P->fb, cnt);
             if (COUNT && first_active_lane()) cnt.c[20] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - r0);

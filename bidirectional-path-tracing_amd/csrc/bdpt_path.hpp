@@ -59,8 +59,10 @@ __device__ __forceinline__ float rr_probability(const DevFrame& fr, int depth, f
 struct LightStore {
     float4* __restrict__ base;
     uint32_t maxv, slot;
+    bool tid_rel = false;  // slot is the block's first; the lane adds threadIdx.x at each access (opaque_tid)
     __device__ __forceinline__ float4* at(int v) const {
-        return base + (static_cast<size_t>(slot) * maxv + static_cast<uint32_t>(v)) * 4;
+        const uint32_t s = tid_rel ? slot + opaque_tid() : slot;
+        return base + (static_cast<size_t>(s) * maxv + static_cast<uint32_t>(v)) * 4;
     }
 };
 __device__ __forceinline__ LightStore light_store(float* lv, int lv_max, uint32_t slot) {

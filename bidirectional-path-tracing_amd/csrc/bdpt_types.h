@@ -76,6 +76,9 @@ constexpr int kShadeStride = BDPT_SHADE_WIDE ? 8 : 5;
 constexpr int kShadeV0 = 5;  // slot of (v0, 0) in a wide record
 
 constexpr uint32_t kLeafBit = 0x80000000u;
+// Words per lane slot of the BDPT megakernel's MT19937 ring (DevScene::mt_ring):
+// the 624-word ring and the generate-ahead cursor (bdpt_device.hpp, mt_ring_ahead).
+constexpr uint32_t kMtRingSlotWords = 640;
 inline uint32_t make_leaf_link(uint32_t start, uint32_t count) { return kLeafBit | (start << 3) | count; }
 
 }  // namespace bdpt
