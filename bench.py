@@ -302,6 +302,8 @@ def main() -> None:
         kernel_ms.append(st["kernel_ms"])
         tail_ms.append(st.get("tail_ms", 0.0))
         capped.append(st.get("capped_samples", 0))
+        if st.get("schedule_errors"):  # a lane-decoupled task without its record, or draws past the generated ring
+            raise RuntimeError(f"{st['schedule_errors']} schedule errors in the render")
         if args.integrator == "path":
             integ.check_levels()  # a sample past the 512-level stack would not be the reference's
         if world > 1:  # the exchange step, timed on its own (host wall: it includes waiting for slower ranks)
