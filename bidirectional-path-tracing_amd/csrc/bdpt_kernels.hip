@@ -172,6 +172,13 @@ struct KParams {
 #ifndef BDPT_TID_REMAT
 #define BDPT_TID_REMAT 1  // the lane's traversal-stack and light-vertex addresses re-derived from threadIdx.x at each use
 #endif
+// The lane's rank among the set lanes of m below it (mbcnt: no per-lane mask
+// held across the loop), and "this is lane 0" from an opaque threadIdx.x.
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
+}
+__device__ __forceinline__ bool lane0() { return (opaque_tid() & 63) == 0; }
 #ifndef BDPT_TAIL_CHUNK
 #define BDPT_TAIL_CHUNK 4  // x the grid's lanes from the end: finer claims (0: 64-sample chunks throughout)
 #endif
@@ -195,7 +202,6 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     if (!FULL) root_lds_fill(root_lds, kp.sc);
 #endif
     scene_tables_to_lds(kp.sc);
-    const int lane = threadIdx.x & 63;
 #if BDPT_TID_REMAT
     const Stack stk{stack_mem, kBlock, kLdsStack, kp.gstack, kp.nslots, blockIdx.x * kBlock, true};
 #else
@@ -225,7 +231,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #if BDPT_EYE_SLOTS
     static_assert(kBlock == 64 * kEyeSlotWaves, "one eye-slot row per wave");
     uint32_t chunk_seq = 0;  // wave-uniform: chunks claimed so far (their eye slot: seq mod BDPT_EYE_SLOTS)
-    if (lane == 0)
+    if (lane0())
         for (int k = 0; k < BDPT_EYE_SLOTS; k++) wave_eye_slots()[k] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
 #endif
 #endif
@@ -250,7 +256,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
     // the kernel's timeline (DevFrame::diag), read through the parameter block
     // where it is stamped (a pointer held across the loop costs SGPR spills)
-    if (BDPT_DIAG && kp.fr.diag && lane == 0) gmin(kp.fr.diag + kDiagStart, __builtin_amdgcn_s_memrealtime());
+    if (BDPT_DIAG && kp.fr.diag && lane0()) gmin(kp.fr.diag + kDiagStart, __builtin_amdgcn_s_memrealtime());
     for (;;) {
         // Re-derived every iteration (opaque to the optimiser) so constants are
         // read where they are used instead of being pinned in registers; typed
@@ -280,7 +286,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 // 4 samples at a time (any sizes partition [0, total)).
                 const uint64_t want = tail_chunk(chunk_base, total);
                 unsigned long long base = 0;
-                if (lane == 0) base = gadd(work, static_cast<unsigned long long>(want));
+                if (lane0()) base = gadd(work, static_cast<unsigned long long>(want));
 #if BDPT_CLAIM_SCALAR
                 // wave-uniform in scalar registers (a shuffle's result is a VGPR pair)
                 base = static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base))) |
@@ -297,20 +303,20 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 chunk_n = static_cast<int>(total - base < want ? total - base : want);
                 chunk_pos = 0;
                 global_done = base + want >= total;
-                if (BDPT_DIAG && global_done && lane == 0 && P->fr.diag)  // the frame's last chunk (one wave claims it)
+                if (BDPT_DIAG && global_done && lane0() && P->fr.diag)  // the frame's last chunk (one wave claims it)
                     P->fr.diag[kDiagLastClaim] = __builtin_amdgcn_s_memrealtime();
                 int px;
-                chunk_x397 = mt_x397(sample_seed(base + lane, P->fr, px));
+                chunk_x397 = mt_x397(sample_seed(base + (opaque_tid() & 63), P->fr, px));
 #if BDPT_EYE_SLOTS
                 // the chunk's pixel when all 64 samples share one (spp a multiple of 64)
                 const int cpx = __shfl(px, 0);
-                if (lane == 0)
+                if (lane0())
                     eye_slot_reset(P->fb, static_cast<int>(chunk_seq % BDPT_EYE_SLOTS), P->fr.spp % 64 == 0 ? cpx : -1);
                 chunk_seq++;
 #endif
             }
             const int m = min(__popcll(idle), chunk_n - chunk_pos);
-            const int rank = __popcll(idle & ((1ull << lane) - 1ull));
+            const int rank = lanes_below(idle);
             const uint32_t x397 = __shfl(chunk_x397, (chunk_pos + rank) & 63);
             if (L.state == ST_IDLE && rank < m) start_sample<true>(L, chunk_base + chunk_pos + rank, P->fr, x397);
             chunk_pos += m;
@@ -322,10 +328,10 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 const int n = __popcll(idle);
                 const int leader = __ffsll(static_cast<unsigned long long>(idle)) - 1;
                 unsigned long long base = 0;
-                if (lane == leader) base = gadd(work, static_cast<unsigned long long>(n));
+                if ((opaque_tid() & 63) == static_cast<uint32_t>(leader)) base = gadd(work, static_cast<unsigned long long>(n));
                 base = __shfl(base, leader);
                 if (L.state == ST_IDLE) {
-                    const uint64_t s = base + __popcll(idle & ((1ull << lane) - 1ull));
+                    const uint64_t s = base + lanes_below(idle);
                     if (s < total) start_sample(L, s, P->fr);
                 }
                 if (base + n >= total) exhausted = true;
@@ -436,12 +442,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
     }
 #if BDPT_SEED_CHUNK && BDPT_EYE_SLOTS
-    if (lane == 0)  // every sample of the wave has finished: the slots' sums to the framebuffer
+    if (lane0())  // every sample of the wave has finished: the slots' sums to the framebuffer
         for (int k = 0; k < BDPT_EYE_SLOTS; k++) eye_slot_reset(kp.fb, k, -1);
 #endif
-    if (BDPT_DIAG && lane == 0 && kpp->fr.diag) gmax(kpp->fr.diag + kDiagEnd, __builtin_amdgcn_s_memrealtime());
+    if (BDPT_DIAG && lane0() && kpp->fr.diag) gmax(kpp->fr.diag + kDiagEnd, __builtin_amdgcn_s_memrealtime());
     if (COUNT) {
-        if (lane == 0) cnt.c[14] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - clock0);
+        if (lane0()) cnt.c[14] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - clock0);
         flush_counts(cnt, kp.counters);
     }
 }
