@@ -291,7 +291,7 @@ def main() -> None:
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    kernel_ms, reduce_ms, tail_ms, capped = [], [], [], []
+    kernel_ms, reduce_ms, tail_ms, capped, parked = [], [], [], [], []
 
     row_offset, row_stride = bdpt_dist.row_shard(rank, world)
 
@@ -302,6 +302,7 @@ def main() -> None:
         kernel_ms.append(st["kernel_ms"])
         tail_ms.append(st.get("tail_ms", 0.0))
         capped.append(st.get("capped_samples", 0))
+        parked.append(st.get("parked_samples", 0))
         if st.get("schedule_errors"):  # a lane-decoupled task without its record, or draws past the generated ring
             raise RuntimeError(f"{st['schedule_errors']} schedule errors in the render")
         if args.integrator == "path":
@@ -318,6 +319,7 @@ def main() -> None:
     reduce_ms.clear()
     tail_ms.clear()
     capped.clear()
+    parked.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -369,7 +371,10 @@ def main() -> None:
         print(json.dumps(out), flush=True)
     elif rank == 0:
         # algorithmic bytes per sample from a counting pass (untimed, same seeds, smaller spp)
-        cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=min(spp, 16), rr_depth=rr,
+        # (Russian roulette: 1 spp — the counting pass keeps every walk in the megakernel,
+        # so a trapped subpath's chain there runs at the lone lane's pace)
+        cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=1 if args.russian_roulette else min(spp, 16),
+                                  rr_depth=rr,
                                   russian_roulette=rrm)
         cnt = bdpt_amd.BDPTIntegrator(integ.scene, cnt_cfg, device=gpu if world > 1 else 0)
         cbuf = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
@@ -452,6 +457,9 @@ def main() -> None:
             # samples that met the store / bounce bounds (must be 0) and the counting pass's maxima
             out["config"]["russian_roulette"] = "NO_RR = 0 (bdpt.h:18)"
             out["russian_roulette"] = {"capped_samples_per_step": capped, "counting_pass_spp": cnt_cfg.spp,
+                                       "parked_walks_per_step": parked,
+                                       "continuation": "walks past BDPT_PARK_DEPTH bounces finished by the chain kernel "
+                                                       "(one wave per walk) and resume launches",
                                        "max_light_depth": cst.get("max_light_depth"),
                                        "max_eye_depth": cst.get("max_eye_depth"),
                                        "max_queries_per_sample": cst.get("max_queries"),

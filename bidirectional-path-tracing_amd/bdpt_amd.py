@@ -170,7 +170,8 @@ class _Stats(ctypes.Structure):
                 ("counters", ctypes.c_int64 * len(COUNTER_NAMES)),  # BDPT_NUM_COUNTERS
                 ("capped_samples", ctypes.c_int64), ("span_ms", ctypes.c_double), ("tail_ms", ctypes.c_double),
                 ("max_light_depth", ctypes.c_int64), ("max_eye_depth", ctypes.c_int64),
-                ("max_queries", ctypes.c_int64), ("schedule_errors", ctypes.c_int64), ("sched", ctypes.c_int64 * 4)]
+                ("max_queries", ctypes.c_int64), ("schedule_errors", ctypes.c_int64), ("sched", ctypes.c_int64 * 4),
+                ("parked_samples", ctypes.c_int64)]
 
 
 # Sources that make up the frame kernels' code objects: their hash stamps the
@@ -721,7 +722,7 @@ class BDPTIntegrator:
         return dict(kernel_ms=s.kernel_ms, samples=s.samples, launches=s.launches,
                     counters=dict(zip(COUNTER_NAMES, list(s.counters))), capped_samples=s.capped_samples,
                     span_ms=s.span_ms, tail_ms=s.tail_ms, max_light_depth=s.max_light_depth,
-                    max_eye_depth=s.max_eye_depth, max_queries=s.max_queries, schedule_errors=s.schedule_errors,
+                    max_eye_depth=s.max_eye_depth, max_queries=s.max_queries, schedule_errors=s.schedule_errors, parked_samples=s.parked_samples,
                     sched=dict(zip(("task_clocks", "tasks_popped", "tasks_without_ray", "own_tasks"), list(s.sched))),
                     kernel=(lib().bdpt_last_kernel(self._h) or b"").decode())
 

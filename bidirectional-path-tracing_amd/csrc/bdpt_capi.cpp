@@ -55,6 +55,10 @@ hipError_t launch_frame_rr(const dev::DevScene& sc, const dev::DevFrame& fr, flo
                            uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
                            hipStream_t stream, void* dparams);
 int frame_kernel_blocks_per_cu_rr(size_t dyn_lds);
+// its continuation pass: one wave per sample parked past park_depth bounces (bdpt_kernels.hip, park_lane)
+hipError_t launch_chain_rr(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                           uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
+                           hipStream_t stream, void* dparams);
 // bdpt_kernels_split.hip: the same megakernel for short subpaths (no ST_DEFER step)
 hipError_t launch_frame_split(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf,
                               uint2* gstack, uint32_t nslots, unsigned long long* work, unsigned long long* counters,
@@ -113,6 +117,22 @@ static bool use_split_build(int rr_depth) {
     const char* e = std::getenv("BDPT_SPLIT_MAX_RR");  // read per render (tests force either build)
     return rr_depth <= (e ? std::atoi(e) : kSplitMaxRrDepth);
 }
+// Russian-roulette continuation pass (bdpt_kernels.hip, park_lane): a light or eye
+// walk deeper than BDPT_PARK_DEPTH bounces (default 256; 0: off) leaves the
+// megakernel for the chain kernel (one wave per sample), which walks its delta
+// chain with the whole wave; BDPT_PARK_ROUNDS (default 4) chain + resume rounds
+// follow the frame (the last resume keeps every walk in the megakernel).
+static int park_depth_setting() {
+    const char* e = std::getenv("BDPT_PARK_DEPTH");
+    return e ? std::atoi(e) : 256;
+}
+static int park_rounds_setting() {
+    const char* e = std::getenv("BDPT_PARK_ROUNDS");
+    return e ? std::max(1, std::atoi(e)) : 4;
+}
+// One wave per parked walk (grid-stride beyond): a frame parks ~2 400 walks of
+// ~180 k bounces on average (Caustic 512^2 x 256), which run side by side.
+constexpr int kChainGrid = 8192;
 constexpr int kMaxRrDepth = 1024;  // beyond 28 the megakernel continues MT19937 from an HBM ring
 // Russian roulette (NO_RR = 0): subpaths are unbounded in the reference (a light
 // subpath trapped by total internal reflection in the Caustic sphere was measured
@@ -188,6 +208,7 @@ struct bdpt_ctx {
     size_t pt_levels_f4 = 0;
     uint32_t* pt_ring = nullptr;
     uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28, RR)
+    uint32_t* park = nullptr;     // Russian roulette: continuation records + parked-slot list (DevFrame::park)
     uint32_t* capped = nullptr;   // samples that met the Russian-roulette bounds, per call
     unsigned long long* diag = nullptr;  // the BDPT frame kernel's timeline (dev::kDiag*)
     bool diag_pending = false;    // the last call was a BDPT frame render (diag is its)
@@ -477,7 +498,7 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
                     static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
                     static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state), static_cast<void*>(c->capped),
                     static_cast<void*>(c->diag), static_cast<void*>(c->ev), c->dq_dparams,
-                    static_cast<void*>(c->splat_list)})
+                    static_cast<void*>(c->splat_list), static_cast<void*>(c->park)})
         if (p) (void)hipFree(p);
     if (c->last_use) (void)hipEventDestroy(c->last_use);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -756,8 +777,30 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
         if (rr) {  // never more resident blocks than the slots allocated
             const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_rr(
                                                            4 * static_cast<size_t>(c->sc.lds_words)));
+            const int park_depth = park_depth_setting();
+            const bool park = park_depth > 0 && !(p->flags & BDPT_FLAG_COUNT);
+            if (park) {
+                const size_t words = static_cast<size_t>(c->nslots) * (kParkSlotWords + 1) + 1;
+                if (!c->park) HIP_TRY(hipMalloc(&c->park, words * sizeof(uint32_t)));
+                HIP_TRY(hipMemsetAsync(c->park, 0, words * sizeof(uint32_t), st));
+                fr.park = c->park;
+                fr.park_depth = park_depth;
+                fr.park_flags = dev::kParkOn;
+            }
             HIP_TRY(launch_frame_rr(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
                                     c->dparams));
+            const int rounds = park ? park_rounds_setting() : 0;
+            uint32_t* const list = c->park + static_cast<size_t>(c->nslots) * kParkSlotWords;
+            for (int k = 0; k < rounds; k++) {
+                HIP_TRY(launch_chain_rr(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, kChainGrid, st,
+                                        c->dparams));
+                HIP_TRY(hipMemsetAsync(list, 0, sizeof(uint32_t), st));  // the resume launch parks anew
+                dev::DevFrame fres = fr;
+                fres.park_flags = dev::kParkResume | (k + 1 < rounds ? dev::kParkOn : 0u);
+                HIP_TRY(launch_frame_rr(sc, fres, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
+                                        c->dparams));
+            }
+            launches += 2 * rounds;
             c->last_kernel = "bdpt_frame_kernel_rr";
         } else if (p->rr_depth > kLazyRrDepth) {  // never more resident blocks than the slots allocated
             const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_deep(
@@ -795,7 +838,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
                                  c->dparams));
             c->last_kernel = "bdpt_frame_kernel";
         }
-        launches = 1;
+        launches += 1;
     }
     HIP_TRY(hipEventRecord(c->ev1, st));
     if ((rc = end_use(c, st))) return rc;
@@ -1124,6 +1167,7 @@ int bdpt_get_stats(bdpt_ctx* c, bdpt_stats* out) {
             if (d[dev::kDiagLastClaim] && d[dev::kDiagEnd] >= d[dev::kDiagLastClaim])
                 c->stats.tail_ms = static_cast<double>(d[dev::kDiagEnd] - d[dev::kDiagLastClaim]) * tick_ms;
             c->stats.schedule_errors = static_cast<int64_t>(d[dev::kDiagErrors]);
+            c->stats.parked_samples = static_cast<int64_t>(d[dev::kDiagParked]);
         }
         c->pending_timing = false;
     }

@@ -82,7 +82,7 @@ struct DevScene {
     uint32_t gdepth;  // traversal-stack overflow entries per lane slot (beyond the LDS ones)
 };
 constexpr uint32_t kNoLds = 0xffffffffu;
-constexpr uint32_t kLdsHdr = 4;  // LDS header words: mt_ring (2 words), mt_ring_stride, unused
+constexpr uint32_t kLdsHdr = 4;  // LDS header words: mt_ring (2 words), mt_ring_stride, the block's first lane slot
 
 // Small per-scene tables — BSDF records, emitter records, shape -> emitter
 // map — live in the kernels' dynamic LDS: the divergent shading code reads
@@ -130,7 +130,7 @@ __device__ __forceinline__ void scene_tables_to_lds(const DevScene& sc) {
         g_scene_lds[0] = static_cast<uint32_t>(ring);
         g_scene_lds[1] = static_cast<uint32_t>(ring >> 32);
         g_scene_lds[2] = sc.mt_ring_stride;
-        g_scene_lds[3] = 0u;
+        g_scene_lds[3] = blockIdx.x * blockDim.x;  // the block's first lane slot (mt_ring_slot)
     }
     if (sc.lds_bsdf_off != kNoLds)
         for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) g_scene_lds[kLdsHdr + i] = b[i];
@@ -169,7 +169,15 @@ struct DevFrame {
     // rounded reciprocal (rcp_cr) and division give: per-frame constants the shading bodies
     // would otherwise recompute (~10 instructions each) per splat and per sample
     float inv_spp, inv_pixels;
+    // Russian-roulette continuation pass (bdpt_kernels.hip): per lane slot a
+    // kParkWords record, then the list of parked slots ([0] count); null: off.
+    // park_flags: kParkOn (park walks deeper than park_depth), kParkResume (this
+    // launch resumes the records the chain kernel returned instead of claiming)
+    uint32_t* park;
+    int32_t park_depth;
+    uint32_t park_flags;
 };
+enum : uint32_t { kParkOn = 1u, kParkResume = 2u };
 
 struct Ray {
     f3 o, d;
@@ -346,9 +354,11 @@ __device__ __forceinline__ uint32_t mt_seed_from(uint32_t x, uint32_t i) {
 // generator's cursor (x[g], x[g+1] of the seeding sequence while g < 623, g,
 // the seed whose outputs the ring holds).
 constexpr uint32_t kMtRingWords = kMtRingSlotWords;
+// The lane's slot: header word 3 (the block's first slot; the Russian-roulette
+// chain kernel stores the slot of the sample it continues there) + threadIdx.x.
 __device__ __forceinline__ uint32_t* mt_ring_slot() {
     const uint64_t base = (static_cast<uint64_t>(g_scene_lds[1]) << 32) | g_scene_lds[0];
-    return reinterpret_cast<uint32_t*>(base) + static_cast<size_t>(blockIdx.x * blockDim.x + threadIdx.x) * kMtRingWords;
+    return reinterpret_cast<uint32_t*>(base) + static_cast<size_t>(g_scene_lds[3] + threadIdx.x) * kMtRingWords;
 }
 // Generates outputs up to r.n + BDPT_RING_AHEAD - 1; false if the lane had
 // already drawn past what was generated (a schedule error: the caller reports it).
@@ -789,7 +799,7 @@ struct Counts {
     uint32_t m[3];  // maxima (counting pass): light-subpath depth, eye-subpath depth, queries per sample
     uint32_t q[4];  // lane-decoupled build: task-phase wave clocks, ring tasks popped, tasks without a ray, own tasks
 };
-enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagErrors = 3, kDiagWords = 4 };
+enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagErrors = 3, kDiagParked = 4, kDiagWords = 5 };
 
 // SIMD-efficiency probe: true on the lowest active lane of the wave only.
 __device__ __forceinline__ bool first_active_lane() {
@@ -1060,11 +1070,12 @@ __device__ __forceinline__ bool trav_node(const TravScene& sc, const Ray& r, con
                                           const Stack& stk, Counts& cnt) {
     return trav_node_vals<COUNT, SLACK>(load_wnode(sc.wnodes, ts.link), r, ri, any, ts, stk, cnt);
 }
-template <bool COUNT, bool SLACK>
-__device__ __forceinline__ bool trav_node_vals(const WNode& n, const Ray& r, const RayInv& ri, bool any,
-                                               TravState& ts, const Stack& stk, Counts& cnt) {
-    if (COUNT) cnt.c[2]++;
-    const float far = cull_far(any ? r.max_t : ts.best_t);
+// The four children of a 4-wide node: key = entry distance of each child the
+// walk must visit (box hit, entered before `far`, left after the near cull), +inf
+// otherwise, sorted near-first together with the links (kEmptyLinkDev for none).
+template <bool SLACK>
+__device__ __forceinline__ void node_child_keys(const WNode& n, const Ray& r, const RayInv& ri, float far, float (&key)[4],
+                                                uint32_t (&lnk)[4]) {
     const float4 lk = n.v[kNodeLinks];
 #if BDPT_QNODES
     // plane distance of bound org + q 2^e: fma(q, 2^e / d, (org - o) / d); 2^e / d is exact
@@ -1075,8 +1086,6 @@ __device__ __forceinline__ bool trav_node_vals(const WNode& n, const Ray& r, con
     const float bx = (n.v[0].x - r.o.x) * ri.inv.x, by = (n.v[0].y - r.o.y) * ri.inv.y,
                 bz = (n.v[0].z - r.o.z) * ri.inv.z;
 #endif
-    float key[4];
-    uint32_t lnk[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) {
         const uint32_t l = __float_as_uint((&lk.x)[c]);
@@ -1105,6 +1114,14 @@ __device__ __forceinline__ bool trav_node_vals(const WNode& n, const Ray& r, con
     }
     BDPT_CE(0, 1) BDPT_CE(2, 3) BDPT_CE(0, 2) BDPT_CE(1, 3) BDPT_CE(1, 2)
 #undef BDPT_CE
+}
+template <bool COUNT, bool SLACK>
+__device__ __forceinline__ bool trav_node_vals(const WNode& n, const Ray& r, const RayInv& ri, bool any,
+                                               TravState& ts, const Stack& stk, Counts& cnt) {
+    if (COUNT) cnt.c[2]++;
+    float key[4];
+    uint32_t lnk[4];
+    node_child_keys<SLACK>(n, r, ri, cull_far(any ? r.max_t : ts.best_t), key, lnk);
     if (lnk[0] == kEmptyLinkDev) return false;
     if (lnk[3] != kEmptyLinkDev) stk.put(ts.sp++, lnk[3], key[3]);
     if (lnk[2] != kEmptyLinkDev) stk.put(ts.sp++, lnk[2], key[2]);
@@ -1233,6 +1250,115 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const Ray& r, bool a
 #endif
     bt = ts.best_t, bu = ts.best_u, bv = ts.best_v;
     return ts.best;
+}
+
+// The closest hit of ONE ray (the same in every lane of the wave) walked by the
+// whole wave: each round pops up to 64 pending entries (one per lane) from an
+// LDS stack, tests them (a 4-wide node: node_child_keys; a leaf: wleaf_tests
+// against the best so far), takes the lexicographic minimum (t, reference
+// index) over the lanes and pushes the children far-first. The result is the
+// serial walk's: the minimum over the candidates of every entry the walk cannot
+// cull (the same conservative per-entry tests, cull_far of the best so far), ties
+// to the lowest reference index, accepted only below r.max_t — the order the
+// entries are visited in does not enter it. For the Russian-roulette
+// continuation pass (bdpt_kernels.hip, chain kernel): a trapped subpath's walk
+// takes ~9 rounds instead of ~30 dependent steps. `stack` holds `cap` entries;
+// false if they did not suffice (the caller reports it). With bound < r.max_t
+// only candidates below `bound` are accepted (and entries beyond it culled): a
+// hit found is then the same result — the minimum over all candidates lies below
+// it — and none found (best -1) means the walk must be repeated unbounded.
+__device__ __forceinline__ uint64_t coop_key(float t, int idx) {
+    const uint32_t b = __float_as_uint(t);
+    const uint32_t o = (b & 0x80000000u) ? ~b : (b | 0x80000000u);  // float order as unsigned order
+    return (static_cast<uint64_t>(o) << 32) | static_cast<uint32_t>(idx);
+}
+// A leaf of up to 4 triangles (the triangle tree's kTriLeafMax) for coop_closest:
+// every triangle's loads issued before the first test (wleaf_tests' loop waits
+// for each triangle in turn); the same acceptance rule, so the same minimum.
+__device__ __forceinline__ void coop_leaf(const TravScene& sc, uint32_t link, const Ray& r, const RayInv& ri, float& bt,
+                                          int& bb, float& bu, float& bv) {
+    const uint32_t start = (link >> 3) & 0x0fffffffu, count = link & 7u;
+    Counts cnt;  // (not a counting pass)
+    if (count > 4) {
+        wleaf_tests<false>(sc.wtri, sc.lbox, link, r, ri, false, bt, bb, bu, bv, cnt);
+        return;
+    }
+    float4 q[4][3];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++)
+        if (k < count) {
+            const float4* p = sc.wtri + 3 * static_cast<size_t>(start + k);
+            q[k][0] = gld4(p), q[k][1] = gld4(p + 1), q[k][2] = gld4(p + 2);
+        }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        if (k >= count) break;
+        float t, u, v;
+        if (!tri_test_edges(xyz(q[k][0]), xyz(q[k][1]), xyz(q[k][2]), r, t, u, v)) continue;
+        const int idx = __float_as_int(q[k][0].w);
+        if ((t < bt || (t == bt && bb >= 0 && idx < bb)) &&
+            ref_leaf_passes<false>(sc.lbox, __float_as_uint(q[k][1].w), r, ri, cnt))
+            bt = t, bb = idx, bu = u, bv = v;
+    }
+}
+
+template <bool SLACK>
+__device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, const RayInv& ri, float bound, uint2* stack,
+                                             int cap, float& best_t, int& best, float& best_u, float& best_v,
+                                             uint32_t* rounds = nullptr) {
+    typedef __attribute__((address_space(3))) u32x2 lds_e;
+    lds_e* const stk = (lds_e*)stack;
+    const uint32_t lane = __lane_id();
+    best_t = bound < r.max_t ? bound : r.max_t, best = -1, best_u = best_v = 0.f;
+    if (lane == 0) stk[0] = u32x2{sc.wroot_link, __float_as_uint(-__builtin_inff())};
+    int sp = 1;
+    bool ok = true;
+    while (sp > 0) {
+        if (rounds) (*rounds)++;
+        const int k = sp < 64 ? sp : 64;
+        u32x2 e = {kEmptyLinkDev, 0u};
+        if (static_cast<int>(lane) < k) e = stk[sp - k + static_cast<int>(lane)];
+        sp -= k;
+        const float far = cull_far(best_t);
+        const bool live = e.x != kEmptyLinkDev && !(__uint_as_float(e.y) > far);
+        float lt = best_t, lu = best_u, lv = best_v;
+        int lb = best;
+        float key[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+        uint32_t lnk[4] = {kEmptyLinkDev, kEmptyLinkDev, kEmptyLinkDev, kEmptyLinkDev};
+        if (live) {
+            if (e.x & kLeafBit) coop_leaf(sc, e.x, r, ri, lt, lb, lu, lv);
+            else node_child_keys<SLACK>(load_wnode(sc.wnodes, e.x), r, ri, far, key, lnk);
+        }
+        // the wave's lexicographic minimum of (t, index) over the lanes that found
+        // a better hit (usually none or one): a scalar loop over their keys
+        uint64_t imp = __ballot(lb != best);
+        if (imp) {
+            uint64_t m = ~0ull;
+            int w = 0;
+            while (imp) {
+                const int i = __ffsll(static_cast<unsigned long long>(imp)) - 1;
+                imp &= imp - 1;
+                const uint64_t ki = coop_key(__shfl(lt, i), __shfl(lb, i));
+                if (ki < m) m = ki, w = i;
+            }
+            best_t = __shfl(lt, w), best = __shfl(lb, w), best_u = __shfl(lu, w), best_v = __shfl(lv, w);
+        }
+        // children far-first, so the nearest are popped first
+#pragma unroll
+        for (int c = 3; c >= 0; c--) {
+            const uint64_t has = __ballot(lnk[c] != kEmptyLinkDev);
+            const int pos = sp + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                     static_cast<uint32_t>(has >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(has), 0u)));
+            const int n = __popcll(has);
+            if (sp + n > cap) {
+                ok = false;
+            } else if (lnk[c] != kEmptyLinkDev) {
+                stk[pos] = u32x2{lnk[c], __float_as_uint(key[c])};
+            }
+            if (sp + n <= cap) sp += n;
+        }
+    }
+    return ok;
 }
 
 // AcceleratorBVH::intersect's shading of a closest hit (accel.h:133-166).

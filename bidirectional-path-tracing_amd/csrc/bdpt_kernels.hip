@@ -128,6 +128,88 @@ __device__ __noinline__ bool express_walk(Lane& Lcaller, const DevScene& sc, con
 }
 #endif
 
+#ifndef BDPT_PARK
+#define BDPT_PARK (BDPT_RR == 1 && !BDPT_SAMPLER_STATE)  // the Russian-roulette continuation pass (below)
+#endif
+#if BDPT_PARK
+// Russian-roulette continuation pass. A subpath trapped in glass by total
+// internal reflection is a serial chain of up to millions of delta bounces
+// (DESIGN.md §8); in the megakernel each of them is one lane's walk at ~30
+// dependent steps. A lane whose light or eye walk passes fr.park_depth bounces
+// saves its sample (registers and cold state; its light vertices and MT19937
+// ring stay in its slot) and stops taking samples; after the frame, the chain
+// kernel continues every saved sample with one wave per sample — the closest
+// hit walked by all 64 lanes (coop_closest), the delta bounce itself on lane 0
+// — until the chain reaches a vertex the megakernel must shade (a miss, a
+// non-delta or emitting hit) or the subpath ends; a resume launch of the
+// megakernel on the same grid then continues each sample in its own slot. The
+// same functions in the same order (express_walk's bounce), so the same bits.
+constexpr uint32_t kParkWords = kParkSlotWords;
+enum : uint32_t {
+    kParkStatus = 0,        // 0 none, 1 parked, 2 returned by the chain kernel
+    kParkResumeDepth = 1,   // the subpath depth at the last resume (a resumed walk parks again D bounces later)
+    kParkRng = 2,           // LazyMT (4)
+    kParkState = 6,
+    kParkRay = 7,           // o, d, min_t, max_t (8)
+    kParkHit = 15,          // p, wo, n, dist, mat, shape (12)
+    kParkCold = 27,         // LaneCold (23)
+};
+static_assert(kParkCold + sizeof(LaneCold) / 4 <= kParkWords, "park record");
+__device__ __forceinline__ uint32_t* park_record(const DevFrame& fr, uint32_t slot) {
+    return fr.park + static_cast<size_t>(slot) * kParkWords;
+}
+__device__ __forceinline__ uint32_t* park_list(const DevFrame& fr, uint32_t nslots) {
+    return fr.park + static_cast<size_t>(nslots) * kParkWords;
+}
+__device__ __forceinline__ void park_save(uint32_t* rec, const Lane& L) {
+    const uint32_t w[kParkCold - kParkRng] = {
+        L.rng.a0, L.rng.a1, L.rng.b, L.rng.n, L.state,
+        __float_as_uint(L.ray.o.x), __float_as_uint(L.ray.o.y), __float_as_uint(L.ray.o.z),
+        __float_as_uint(L.ray.d.x), __float_as_uint(L.ray.d.y), __float_as_uint(L.ray.d.z),
+        __float_as_uint(L.ray.min_t), __float_as_uint(L.ray.max_t),
+        __float_as_uint(L.h.p.x), __float_as_uint(L.h.p.y), __float_as_uint(L.h.p.z),
+        __float_as_uint(L.h.wo.x), __float_as_uint(L.h.wo.y), __float_as_uint(L.h.wo.z),
+        __float_as_uint(L.h.n.x), __float_as_uint(L.h.n.y), __float_as_uint(L.h.n.z),
+        __float_as_uint(L.h.dist), static_cast<uint32_t>(L.h.mat), static_cast<uint32_t>(L.h.shape)};
+    gbl_u32* const g = (gbl_u32*)rec;
+#pragma unroll
+    for (uint32_t k = 0; k < kParkCold - kParkRng; k++) g[kParkRng + k] = w[k];
+    const uint32_t* c = reinterpret_cast<const uint32_t*>(&L.c);
+#pragma unroll
+    for (uint32_t k = 0; k < sizeof(LaneCold) / 4; k++) g[kParkCold + k] = c[k];
+}
+__device__ __forceinline__ void park_restore(const uint32_t* rec, Lane& L) {
+    const gbl_u32* const g = (const gbl_u32*)rec;
+    L.rng = LazyMT{g[kParkRng], g[kParkRng + 1], g[kParkRng + 2], g[kParkRng + 3]};
+    L.state = g[kParkState];
+    const float* r = reinterpret_cast<const float*>(rec + kParkRay);
+    L.ray = Ray{mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], r[7]};
+    const float* h = reinterpret_cast<const float*>(rec + kParkHit);
+    L.h.p = mk(h[0], h[1], h[2]), L.h.wo = mk(h[3], h[4], h[5]), L.h.n = mk(h[6], h[7], h[8]);
+    L.h.dist = h[9], L.h.mat = static_cast<int>(g[kParkHit + 10]), L.h.shape = static_cast<int>(g[kParkHit + 11]);
+    uint32_t* c = reinterpret_cast<uint32_t*>(&L.c);
+#pragma unroll
+    for (uint32_t k = 0; k < sizeof(LaneCold) / 4; k++) c[k] = g[kParkCold + k];
+}
+// The lane's sample leaves the megakernel here (the query it was about to walk
+// is the chain kernel's first).
+__device__ __forceinline__ bool park_lane(const DevFrame& fr, uint32_t nslots, uint32_t slot, const Lane& L) {
+    uint32_t* const rec = park_record(fr, slot);
+    if ((fr.park_flags & kParkResume) && !(L.c.depth > static_cast<int>(((const gbl_u32*)rec)[kParkResumeDepth]) + fr.park_depth))
+        return false;  // resumed: D more bounces first
+    park_save(rec, L);
+    ((gbl_u32*)rec)[kParkStatus] = 1u;
+    uint32_t* const list = park_list(fr, nslots);
+    const uint32_t k = gadd(list, 1u);
+    ((gbl_u32*)list)[1 + k] = slot;
+    if (fr.diag) gadd(fr.diag + kDiagParked, 1ull);
+    return true;
+}
+#define BDPT_BUSY(st) ((st) != ST_IDLE && (st) != ST_PARKED)
+#else
+#define BDPT_BUSY(st) ((st) != ST_IDLE)
+#endif
+
 // One query for the lane's pending state, then the state advance.
 template <bool FULL, bool COUNT>
 __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
@@ -223,6 +305,17 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     Lane L(cold_mem[threadIdx.x]);
     L.state = ST_IDLE;
     bool exhausted = false;  // wave-uniform
+#if BDPT_PARK
+    if (kp.fr.park_flags & kParkResume) {  // a resume launch: the chain kernel's samples, no claims
+        exhausted = true;
+        gbl_u32* const rec = (gbl_u32*)park_record(kp.fr, blockIdx.x * kBlock + threadIdx.x);
+        if (rec[kParkStatus] == 2u) {
+            park_restore((const uint32_t*)rec, L);
+            rec[kParkStatus] = 0u;
+            rec[kParkResumeDepth] = static_cast<uint32_t>(L.c.depth);
+        }
+    }
+#endif
 #if BDPT_SEED_CHUNK
     uint64_t chunk_base = 0;  // wave-uniform: the wave's current chunk of samples
     int chunk_pos = 0, chunk_n = 0;
@@ -338,7 +431,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             }
         }
 #endif
-        if (__ballot(L.state != ST_IDLE) == 0) {
+        if (__ballot(BDPT_BUSY(L.state)) == 0) {
             if (exhausted) break;
             continue;
         }
@@ -349,7 +442,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // while the slow walkers resume afterwards from where they stopped.
 #if BDPT_RR == 1 && BDPT_EXPRESS_WALK
         if (!COUNT && express) {  // a trapped subpath alone in its wave: its delta chain out of line
-            const bool alone = __popcll(__ballot(L.state != ST_IDLE)) == 1;
+            const bool alone = __popcll(__ballot(BDPT_BUSY(L.state))) == 1;
             if (alone && !tracing && !has_res && (L.state == ST_LIGHT || L.state == ST_EYE)) {
                 if (express_walk(L, P->sc, P->fr, P->fb, stk, res, rt, ru, rv)) has_res = true;
                 if (!has_res) {
@@ -359,7 +452,14 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             }
         }
 #endif
-        if (L.state != ST_IDLE && !tracing && !has_res) {  // a new query: begin its walk
+#if BDPT_PARK
+        if (!COUNT && (P->fr.park_flags & kParkOn) && !tracing && !has_res && (L.state == ST_LIGHT || L.state == ST_EYE) &&
+            L.c.depth > P->fr.park_depth && park_lane(P->fr, P->nslots, blockIdx.x * kBlock + opaque_tid(), L)) {
+            L.state = ST_PARKED;
+            long_walk = false;
+        }
+#endif
+        if (BDPT_BUSY(L.state) && !tracing && !has_res) {  // a new query: begin its walk
             q_any = is_shadow_state(L.state);
             if (COUNT && L.state != ST_DEFER) cnt.c[q_any ? 1 : 0]++;
             ri = ray_inv(L.ray, cull_near_for(L));
@@ -452,6 +552,137 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     }
 }
 
+
+#if BDPT_PARK
+// The continuation pass's chain kernel: one wave per parked sample (see park_lane).
+#ifndef BDPT_CHAIN_PROBE
+#define BDPT_CHAIN_PROBE 0
+#endif
+#ifndef BDPT_CHAIN_LDS_RING
+#define BDPT_CHAIN_LDS_RING 1  // the chain's MT19937 ring in LDS (each draw an LDS read instead of an HBM round trip)
+#endif
+constexpr int kChainStack = 2048;  // LDS entries of the wave's shared walk stack
+__global__ __launch_bounds__(64) void bdpt_chain_kernel(const KParams* __restrict__ kpp) {
+    const KParams& kp = *kpp;
+    __shared__ uint2 cstack[kChainStack];
+    __shared__ LaneCold cold;
+#if BDPT_CHAIN_LDS_RING
+    __shared__ uint32_t lring[kMtRingSlotWords];
+#endif
+    scene_tables_to_lds(kp.sc);
+    const uint32_t lane = threadIdx.x;
+#if BDPT_EYE_SLOTS
+    if (lane == 0)  // no eye-estimate slots here: a sample that ends adds to the framebuffer itself
+        for (int k = 0; k < BDPT_EYE_SLOTS; k++) wave_eye_slots()[k] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+#endif
+    const DevScene& sc = kp.sc;
+    const DevFrame& fr = kp.fr;
+    const TravScene tsc = trav_scene(sc);
+    const gbl_u32* const list = (const gbl_u32*)park_list(fr, kp.nslots);
+    const uint32_t n = list[0];
+    Counts cnt;  // (not a counting pass)
+    // BDPT_CHAIN_PROBE: bounces, walk rounds, walk clocks, chain clocks into bdpt_stats.sched
+    uint64_t pc[4] = {0u, 0u, 0u, 0u};
+    uint32_t rounds32 = 0;
+    uint32_t* const probe_rounds = BDPT_CHAIN_PROBE ? &rounds32 : nullptr;
+    const uint64_t k0 = BDPT_CHAIN_PROBE ? __builtin_amdgcn_s_memtime() : 0;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t slot = list[1 + i];
+        uint32_t* const rec = park_record(fr, slot);
+        Lane L(cold);
+        float guess = -1.f;  // the last hit distance of this chain (wave-uniform)
+#if BDPT_CHAIN_LDS_RING
+        // the slot's MT19937 ring (and generator cursor) in LDS while the chain draws from it
+        gbl_u32* const hring = (gbl_u32*)(sc.mt_ring + static_cast<size_t>(slot) * kMtRingSlotWords);
+        for (uint32_t k = lane; k < kMtRingSlotWords; k += 64) lring[k] = hring[k];
+        if (lane == 0) {
+            const uint64_t a = reinterpret_cast<uint64_t>(static_cast<uint32_t*>(lring));
+            g_scene_lds[0] = static_cast<uint32_t>(a), g_scene_lds[1] = static_cast<uint32_t>(a >> 32);
+            g_scene_lds[3] = 0u;  // mt_ring_slot: lring for lane 0
+            park_restore(rec, L);
+        }
+        __syncthreads();
+#else
+        if (lane == 0) {
+            park_restore(rec, L);
+            g_scene_lds[3] = slot;  // the sample's MT19937 ring (mt_ring_slot, lane 0)
+        }
+#endif
+        for (;;) {
+            const uint64_t c0 = BDPT_CHAIN_PROBE ? __builtin_amdgcn_s_memtime() : 0;
+            // lane 0's query, walked by the wave
+            Ray q;
+            q.o = mk(__shfl(L.ray.o.x, 0), __shfl(L.ray.o.y, 0), __shfl(L.ray.o.z, 0));
+            q.d = mk(__shfl(L.ray.d.x, 0), __shfl(L.ray.d.y, 0), __shfl(L.ray.d.z, 0));
+            q.min_t = __shfl(L.ray.min_t, 0), q.max_t = __shfl(L.ray.max_t, 0);
+            const float near = __shfl(lane == 0 ? cull_near_for(L) : 0.f, 0);
+            if (q.min_t > q.max_t) break;  // the megakernel resolves it (a miss)
+            const RayInv ri = ray_inv(q, near);
+            if (!ri.fast || far_origin(sc, q.o)) break;  // the reference's tree: the megakernel walks it
+            // A chain in glass repeats its chord lengths: the walk first accepts only hits
+            // below twice the last one (culling the boxes beyond), then, if none, unbounded.
+            float t, u, v;
+            int r = -1;
+            bool ok = true;
+            for (int pass = guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
+                const float bound = pass == 0 ? 2.f * guess : q.max_t;
+                ok = tsc.node_slack ? coop_closest<true>(tsc, q, ri, bound, cstack, kChainStack, t, r, u, v, probe_rounds)
+                                    : coop_closest<false>(tsc, q, ri, bound, cstack, kChainStack, t, r, u, v, probe_rounds);
+            }
+            if (BDPT_CHAIN_PROBE) pc[0]++, pc[2] += __builtin_amdgcn_s_memtime() - c0;
+            guess = r >= 0 ? t : -1.f;
+            if (!ok) {
+                if (lane == 0 && fr.diag) gadd(fr.diag + kDiagErrors, 1ull);
+                break;
+            }
+            const bool hit = r >= 0 && t <= q.max_t && t >= q.min_t;  // accel.h:133
+            if (!hit) break;
+            const BsdfRecord& b = bsdf_of(sc, __float_as_int(gld4(sc.shade + kShadeStride * static_cast<size_t>(r)).w));
+            if (!is_delta(b) || !is_zero(ld3(b.emission))) break;  // a vertex the megakernel shades
+            int more = 0;
+            if (lane == 0 && L.c.steps + 1 <= (1 << 30)) {
+                // the sweep's work at a delta, non-emitting vertex (express_walk's bounce): resolve(),
+                // the vertex update (bdpt.h:193-209 / :73-136), ContinuePathRandomWalk, the loop test
+                ++L.c.steps;
+                shade_hit(sc, r, u, v, t, L.ray.d, L.h);
+                const float dist2 = L.h.dist * L.h.dist;
+                BDPT_DIST_TO_GRAZE
+                const float absCosIn = fabsf(L.h.wo.z);
+#if BDPT_RING_AHEAD
+                if (L.rng.n + BDPT_RING_AHEAD >= 227 && !mt_ring_ahead(L.rng) && fr.diag)
+                    gadd(fr.diag + kDiagErrors, 1ull);
+#endif
+                L.c.vcm *= div_cr(dist2, absCosIn);
+                L.c.vc *= rcp_cr(absCosIn);
+                L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);
+                const bool light = L.state == ST_LIGHT;
+                const bool cont = continue_walk(b, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, L.c.rr);
+                if (cont && walk_continues(L, fr)) {
+                    more = 1;
+                } else if (light) {
+                    L.state = ST_DEFER;  // the eye subpath starts in the megakernel's next step
+                } else {
+                    finish<false>(L, fr, kp.fb, cnt);  // L.state = ST_IDLE
+                }
+            }
+            if (!__shfl(more, 0)) break;
+        }
+        if (lane == 0) {
+            park_save(rec, L);
+            ((gbl_u32*)rec)[kParkStatus] = 2u;
+        }
+#if BDPT_CHAIN_LDS_RING
+        __syncthreads();
+        for (uint32_t k = lane; k < kMtRingSlotWords; k += 64) hring[k] = lring[k];
+#endif
+    }
+    if (BDPT_CHAIN_PROBE && lane == 0 && n > blockIdx.x) {
+        pc[1] = rounds32;
+        pc[3] = __builtin_amdgcn_s_memtime() - k0;
+        for (int k = 0; k < 4; k++) gadd(kp.counters + kCounters + 3 + k, static_cast<unsigned long long>(pc[k]));
+    }
+}
+#endif
 #endif  // !BDPT_SAMPLER_STATE
 
 #if BDPT_SAMPLER_STATE
@@ -514,6 +745,21 @@ hipError_t launch_frame(const dev::DevScene& sc, const dev::DevFrame& fr, float*
     return hipGetLastError();
 }
 
+
+#if BDPT_PARK
+// The Russian-roulette continuation pass's chain kernel (one wave per parked
+// sample, grid-stride over the list); same parameter block as launch_frame.
+hipError_t launch_chain(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                        uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
+                        hipStream_t stream, void* dparams) {
+    const dev::KParams host{sc, fr, fb, lvbuf, gstack, nslots, work, counters};
+    hipError_t e = hipMemcpyAsync(dparams, &host, sizeof(host), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(dev::bdpt_chain_kernel, dim3(grid), dim3(64), 4 * static_cast<size_t>(sc.lds_words), stream,
+                       static_cast<const dev::KParams*>(dparams));
+    return hipGetLastError();
+}
+#endif
 #endif  // !BDPT_SAMPLER_STATE
 
 #if BDPT_SAMPLER_STATE

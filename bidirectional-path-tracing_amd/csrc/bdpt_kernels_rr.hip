@@ -11,6 +11,8 @@
 #define bdpt_sample_kernel bdpt_sample_kernel_rr
 #define frame_params_bytes frame_params_bytes_rr
 #define launch_frame launch_frame_rr
+#define launch_chain launch_chain_rr
+#define bdpt_chain_kernel bdpt_chain_kernel_rr
 #define launch_sample launch_sample_rr
 #define frame_kernel_blocks_per_cu frame_kernel_blocks_per_cu_rr
 #define frame_kernel_lds_stack frame_kernel_lds_stack_rr

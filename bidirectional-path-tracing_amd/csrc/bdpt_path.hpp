@@ -200,6 +200,7 @@ enum : uint32_t {  // the query a lane waits on
     ST_NEE,      // connectToLight visibility (bdpt.h:405)
     ST_CONN,     // connectVertices visibility (bdpt.h:451)
     ST_DEFER,    // no query: the lane resumes at A_START_EYE in the next shading step
+    ST_PARKED,   // Russian-roulette build: the sample's deep walk continues in the chain kernel
 };
 enum : uint32_t {  // actions that need no query
     A_ISSUED = 0,

@@ -79,6 +79,9 @@ constexpr uint32_t kLeafBit = 0x80000000u;
 // Words per lane slot of the BDPT megakernel's MT19937 ring (DevScene::mt_ring):
 // the 624-word ring and the generate-ahead cursor (bdpt_device.hpp, mt_ring_ahead).
 constexpr uint32_t kMtRingSlotWords = 640;
+// Words per lane slot of the Russian-roulette continuation records (DevFrame::park;
+// bdpt_kernels.hip, park_save); the list of parked slots follows the records.
+constexpr uint32_t kParkSlotWords = 64;
 inline uint32_t make_leaf_link(uint32_t start, uint32_t count) { return kLeafBit | (start << 3) | count; }
 
 }  // namespace bdpt

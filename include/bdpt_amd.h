@@ -147,11 +147,14 @@ typedef struct {
     int64_t max_light_depth; /* counting pass (BDPT_FLAG_COUNT) maxima over the samples: light-subpath */
     int64_t max_eye_depth;   /* depth, eye-subpath depth, */
     int64_t max_queries;     /* ray queries of one sample */
-    int64_t schedule_errors; /* lane-decoupled build: connection tasks whose descriptor named no record
-                                (skipped; any non-zero count is a bug, and bdpt_render_host fails) */
+    int64_t schedule_errors; /* connection tasks of the lane-decoupled build whose descriptor named no record,
+                                MT19937 draws past the generated ring, a continuation walk out of stack
+                                (any non-zero count is a bug, and bdpt_render_host fails) */
     int64_t sched[4];        /* counting pass of the lane-decoupled build: task-phase wave clocks, tasks
                                 popped from the block rings, tasks that traced no shadow ray, tasks their
                                 owner ran itself (ring full) */
+    int64_t parked_samples;  /* Russian roulette: walks handed to the continuation pass's chain kernel
+                                (deeper than BDPT_PARK_DEPTH bounces; a sample may be handed over again) */
 } bdpt_stats;
 
 const char* bdpt_last_error(void);

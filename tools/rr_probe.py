@@ -48,7 +48,8 @@ for flags, label in passes:
     st = it.stats()  # waits for the kernel
     out = {"pass": label, "scene": name, "W": W, "H": H, "spp": spp, "rows": [off, stride], "samples": st["samples"],
            "kernel_ms": round(st["kernel_ms"], 3), "span_ms": round(st["span_ms"], 3),
-           "tail_ms": round(st["tail_ms"], 3), "capped": st["capped_samples"], "wall_s": round(time.time() - t, 3),
+           "tail_ms": round(st["tail_ms"], 3), "capped": st["capped_samples"],
+           "parked": st.get("parked_samples"), "launches": st.get("launches"), "sched": st.get("sched"), "wall_s": round(time.time() - t, 3),
            "kernel": st["kernel"]}
     if flags:
         out.update(max_light_depth=st["max_light_depth"], max_eye_depth=st["max_eye_depth"],
