@@ -1302,22 +1302,33 @@ __device__ __forceinline__ void coop_leaf(const TravScene& sc, uint32_t link, co
     }
 }
 
-template <bool SLACK>
-__device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, const RayInv& ri, float bound, uint2* stack,
-                                             int cap, float& best_t, int& best, float& best_u, float& best_v,
-                                             uint32_t* rounds = nullptr) {
-    typedef __attribute__((address_space(3))) u32x2 lds_e;
-    lds_e* const stk = (lds_e*)stack;
+// The walk's LDS stack: entry e at base[e] (a wave's own array), or spread over
+// the columns a wave's lanes own in a block's per-lane stack (entry e at
+// base[(e / 64) * stride + e % 64], base = the wave's first lane).
+typedef __attribute__((address_space(3))) u32x2 coop_lds_e;
+struct CoopStack {
+    uint2* base;
+    int stride;  // 0: contiguous
+    __device__ __forceinline__ coop_lds_e* at(int e) const {
+        return (coop_lds_e*)base + (stride ? (e >> 6) * stride + (e & 63) : e);
+    }
+};
+// BATCH: coop_leaf (a leaf's triangle loads issued together, 48 more live
+// registers) rather than wleaf_tests.
+template <bool SLACK, bool BATCH = true>
+__device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, const RayInv& ri, float bound,
+                                             CoopStack stk, int cap, float& best_t, int& best, float& best_u,
+                                             float& best_v, uint32_t* rounds = nullptr) {
     const uint32_t lane = __lane_id();
     best_t = bound < r.max_t ? bound : r.max_t, best = -1, best_u = best_v = 0.f;
-    if (lane == 0) stk[0] = u32x2{sc.wroot_link, __float_as_uint(-__builtin_inff())};
+    if (lane == 0) *stk.at(0) = u32x2{sc.wroot_link, __float_as_uint(-__builtin_inff())};
     int sp = 1;
     bool ok = true;
     while (sp > 0) {
         if (rounds) (*rounds)++;
         const int k = sp < 64 ? sp : 64;
         u32x2 e = {kEmptyLinkDev, 0u};
-        if (static_cast<int>(lane) < k) e = stk[sp - k + static_cast<int>(lane)];
+        if (static_cast<int>(lane) < k) e = *stk.at(sp - k + static_cast<int>(lane));
         sp -= k;
         const float far = cull_far(best_t);
         const bool live = e.x != kEmptyLinkDev && !(__uint_as_float(e.y) > far);
@@ -1326,7 +1337,14 @@ __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, 
         float key[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
         uint32_t lnk[4] = {kEmptyLinkDev, kEmptyLinkDev, kEmptyLinkDev, kEmptyLinkDev};
         if (live) {
-            if (e.x & kLeafBit) coop_leaf(sc, e.x, r, ri, lt, lb, lu, lv);
+            if (e.x & kLeafBit) {
+                if (BATCH) {
+                    coop_leaf(sc, e.x, r, ri, lt, lb, lu, lv);
+                } else {
+                    Counts cnt;  // (not a counting pass)
+                    wleaf_tests<false>(sc.wtri, sc.lbox, e.x, r, ri, false, lt, lb, lu, lv, cnt);
+                }
+            }
             else node_child_keys<SLACK>(load_wnode(sc.wnodes, e.x), r, ri, far, key, lnk);
         }
         // the wave's lexicographic minimum of (t, index) over the lanes that found
@@ -1353,7 +1371,7 @@ __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, 
             if (sp + n > cap) {
                 ok = false;
             } else if (lnk[c] != kEmptyLinkDev) {
-                stk[pos] = u32x2{lnk[c], __float_as_uint(key[c])};
+                *stk.at(pos) = u32x2{lnk[c], __float_as_uint(key[c])};
             }
             if (sp + n <= cap) sp += n;
         }

@@ -69,6 +69,12 @@ constexpr int kBlock = 256;
 #define BDPT_ROOT_LDS 1  // 1: the traversal root and its interior children in LDS, tested when a walk begins (RootLds; measured +1.6 %)
 #endif
 
+#ifndef BDPT_COOP_ALONE
+#define BDPT_COOP_ALONE (BDPT_RR == 1 && !BDPT_SAMPLER_STATE)  // a lone trapped walk walked by its whole wave (below)
+#endif
+#ifndef BDPT_COOP_BATCH
+#define BDPT_COOP_BATCH 0  // the megakernel's wave walk tests leaves with wleaf_tests (coop_leaf's batched loads cost spills)
+#endif
 #ifndef BDPT_EXPRESS_WALK
 #define BDPT_EXPRESS_WALK 0  // 1: a lone trapped lane's delta chain out of line (express_walk; 1.5 % faster on the trapped chain, +49 VGPR spills in the RR build)
 #endif
@@ -129,7 +135,7 @@ __device__ __noinline__ bool express_walk(Lane& Lcaller, const DevScene& sc, con
 #endif
 
 #ifndef BDPT_PARK
-#define BDPT_PARK (BDPT_RR == 1 && !BDPT_SAMPLER_STATE)  // the Russian-roulette continuation pass (below)
+#define BDPT_PARK (BDPT_RR == 1 && !BDPT_SAMPLER_STATE)  // the Russian-roulette continuation pass (below; opt-in per render)
 #endif
 #if BDPT_PARK
 // Russian-roulette continuation pass. A subpath trapped in glass by total
@@ -343,6 +349,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     // the trapped lane advances one bounce per walk instead of one per shared
     // shading step (the frame cannot end before it does).
     bool long_walk = false;
+#if BDPT_COOP_ALONE
+    float coop_guess = -1.f;  // wave-uniform: the last hit distance of the wave's lone trapped walk
+#endif
     const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
 #ifndef BDPT_DIAG
 #define BDPT_DIAG 1  // 0: no timeline stamps (A/B only)
@@ -459,6 +468,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             long_walk = false;
         }
 #endif
+#if BDPT_COOP_ALONE
+        bool began = false;  // this lane began a culled closest-hit walk in this iteration
+#endif
         if (BDPT_BUSY(L.state) && !tracing && !has_res) {  // a new query: begin its walk
             q_any = is_shadow_state(L.state);
             if (COUNT && L.state != ST_DEFER) cnt.c[q_any ? 1 : 0]++;
@@ -477,6 +489,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             } else {
                 ts = trav_begin(tsc, L.ray);
                 tracing = true;
+#if BDPT_COOP_ALONE
+                began = !q_any;
+#endif
 #if BDPT_ROOT_LDS
                 if (root_in_lds && !walk_begin_lds<COUNT, SLACK>(root_lds, L.ray, ri, q_any, ts, stk, cnt)) {
                     res = -1, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;  // no child hit: a miss
@@ -486,6 +501,46 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
             }
         }
+#if BDPT_COOP_ALONE
+        // A subpath trapped in glass alone in its wave (express mode): the wave walks
+        // its closest hit together (coop_closest: ~10 rounds instead of ~30 steps)
+        // on the LDS stack columns of its lanes; bounded by twice the last hit
+        // first (a chain in glass repeats its chord lengths). If the columns do
+        // not suffice, the lane walks alone from the root.
+        if (!COUNT && express) {
+            const uint64_t busy = __ballot(BDPT_BUSY(L.state));
+            if (__popcll(busy) == 1 && __ballot(began) == busy) {
+                const int b = __ffsll(static_cast<unsigned long long>(busy)) - 1;
+                Ray q;
+                q.o = mk(__shfl(L.ray.o.x, b), __shfl(L.ray.o.y, b), __shfl(L.ray.o.z, b));
+                q.d = mk(__shfl(L.ray.d.x, b), __shfl(L.ray.d.y, b), __shfl(L.ray.d.z, b));
+                q.min_t = __shfl(L.ray.min_t, b), q.max_t = __shfl(L.ray.max_t, b);
+                RayInv qi;
+                qi.inv = mk(__shfl(ri.inv.x, b), __shfl(ri.inv.y, b), __shfl(ri.inv.z, b));
+                qi.near = __shfl(ri.near, b);
+                qi.fast = true;
+                const CoopStack cs{stack_mem + (threadIdx.x & ~63u), kBlock};
+                float t = 0.f, u = 0.f, v = 0.f;
+                int r = -1;
+                bool ok = true;
+                for (int pass = coop_guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
+                    const float bound = pass == 0 ? 2.f * coop_guess : q.max_t;
+                    ok = SLACK ? coop_closest<true, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v)
+                               : coop_closest<false, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v);
+                }
+                coop_guess = ok && r >= 0 ? t : -1.f;
+                if (began) {
+                    if (ok) {
+                        res = r, rt = t, ru = u, rv = v;
+                        tracing = false;
+                        has_res = true;
+                    } else {
+                        ts = trav_begin(tsc, L.ray);  // its stack columns were the wave's
+                    }
+                }
+            }
+        }
+#endif
         const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
         for (;;) {  // walk until enough lanes have a result to shade
             const uint64_t tr = __ballot(tracing);
@@ -581,7 +636,7 @@ __global__ __launch_bounds__(64) void bdpt_chain_kernel(const KParams* __restric
     const gbl_u32* const list = (const gbl_u32*)park_list(fr, kp.nslots);
     const uint32_t n = list[0];
     Counts cnt;  // (not a counting pass)
-    // BDPT_CHAIN_PROBE: bounces, walk rounds, walk clocks, chain clocks into bdpt_stats.sched
+    // BDPT_CHAIN_PROBE: bounces, walk rounds, and the longest walk's bounces and clocks into bdpt_stats.sched
     uint64_t pc[4] = {0u, 0u, 0u, 0u};
     uint32_t rounds32 = 0;
     uint32_t* const probe_rounds = BDPT_CHAIN_PROBE ? &rounds32 : nullptr;
@@ -591,6 +646,7 @@ __global__ __launch_bounds__(64) void bdpt_chain_kernel(const KParams* __restric
         uint32_t* const rec = park_record(fr, slot);
         Lane L(cold);
         float guess = -1.f;  // the last hit distance of this chain (wave-uniform)
+        const uint64_t w0 = BDPT_CHAIN_PROBE ? __builtin_amdgcn_s_memtime() : 0, wb = pc[0];
 #if BDPT_CHAIN_LDS_RING
         // the slot's MT19937 ring (and generator cursor) in LDS while the chain draws from it
         gbl_u32* const hring = (gbl_u32*)(sc.mt_ring + static_cast<size_t>(slot) * kMtRingSlotWords);
@@ -626,8 +682,9 @@ __global__ __launch_bounds__(64) void bdpt_chain_kernel(const KParams* __restric
             bool ok = true;
             for (int pass = guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
                 const float bound = pass == 0 ? 2.f * guess : q.max_t;
-                ok = tsc.node_slack ? coop_closest<true>(tsc, q, ri, bound, cstack, kChainStack, t, r, u, v, probe_rounds)
-                                    : coop_closest<false>(tsc, q, ri, bound, cstack, kChainStack, t, r, u, v, probe_rounds);
+                const CoopStack cs{cstack, 0};
+                ok = tsc.node_slack ? coop_closest<true>(tsc, q, ri, bound, cs, kChainStack, t, r, u, v, probe_rounds)
+                                    : coop_closest<false>(tsc, q, ri, bound, cs, kChainStack, t, r, u, v, probe_rounds);
             }
             if (BDPT_CHAIN_PROBE) pc[0]++, pc[2] += __builtin_amdgcn_s_memtime() - c0;
             guess = r >= 0 ? t : -1.f;
@@ -670,6 +727,10 @@ __global__ __launch_bounds__(64) void bdpt_chain_kernel(const KParams* __restric
         if (lane == 0) {
             park_save(rec, L);
             ((gbl_u32*)rec)[kParkStatus] = 2u;
+            if (BDPT_CHAIN_PROBE) {  // the longest walk: its bounces and clocks
+                gmax(kp.counters + kCounters + 3 + 2, static_cast<unsigned long long>(pc[0] - wb));
+                gmax(kp.counters + kCounters + 3 + 3, static_cast<unsigned long long>(__builtin_amdgcn_s_memtime() - w0));
+            }
         }
 #if BDPT_CHAIN_LDS_RING
         __syncthreads();
@@ -677,10 +738,10 @@ __global__ __launch_bounds__(64) void bdpt_chain_kernel(const KParams* __restric
 #endif
     }
     if (BDPT_CHAIN_PROBE && lane == 0 && n > blockIdx.x) {
-        pc[1] = rounds32;
-        pc[3] = __builtin_amdgcn_s_memtime() - k0;
-        for (int k = 0; k < 4; k++) gadd(kp.counters + kCounters + 3 + k, static_cast<unsigned long long>(pc[k]));
+        gadd(kp.counters + kCounters + 3, static_cast<unsigned long long>(pc[0]));
+        gadd(kp.counters + kCounters + 3 + 1, static_cast<unsigned long long>(rounds32));
     }
+    (void)k0;
 }
 #endif
 #endif  // !BDPT_SAMPLER_STATE
