@@ -213,6 +213,7 @@ struct bdpt_ctx {
     uint32_t* pt_ring = nullptr;
     uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28, RR)
     uint32_t* park = nullptr;     // Russian roulette: continuation records + parked-slot list (DevFrame::park)
+    unsigned long long work_init = 0;  // BDPT_SAMPLE_RANGE's first sample (host copy for the async upload)
     uint32_t* capped = nullptr;   // samples that met the Russian-roulette bounds, per call
     unsigned long long* diag = nullptr;  // the BDPT frame kernel's timeline (dev::kDiag*)
     bool diag_pending = false;    // the last call was a BDPT frame render (diag is its)
@@ -770,6 +771,16 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     }
     if ((rc = begin_use(c, st))) return rc;
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
+    // BDPT_SAMPLE_RANGE="lo,hi" (debugging aid, tools/rr_find.py): only the shard's
+    // samples [lo, hi) — the work counter starts at lo and the frame ends at hi
+    if (const char* sr = std::getenv("BDPT_SAMPLE_RANGE")) {
+        unsigned long long lo = 0, hi = 0;
+        if (std::sscanf(sr, "%llu,%llu", &lo, &hi) == 2 && lo <= hi) {
+            fr.total_samples = std::min<uint64_t>(fr.total_samples, hi);
+            c->work_init = std::min<unsigned long long>(lo, fr.total_samples);
+            HIP_TRY(hipMemcpyAsync(c->work, &c->work_init, sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+        }
+    }
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kCounterWords, st));
     HIP_TRY(hipMemsetAsync(c->capped, 0, sizeof(uint32_t), st));
     HIP_TRY(hipMemsetAsync(c->diag, 0, sizeof(unsigned long long) * dev::kDiagWords, st));

@@ -91,6 +91,9 @@ def lib():
         L.tro_scene_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
         L.tro_scene_dump.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 4
         L.tro_camera.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p]
+        L.tro_render_row_samples.restype = ctypes.c_int64
+        L.tro_render_row_samples.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.c_int64, ctypes.c_int64]
         L.tro_render.restype = ctypes.c_int64
         L.tro_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_void_p,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -188,6 +191,14 @@ class Scene:
         for f in fbs[1:]:
             fb += f
         return fb, sum(counts)
+
+    def render_row_samples(self, p: Params, row: int, s_lo: int, s_hi: int, fb: np.ndarray | None = None) -> np.ndarray:
+        """Samples [s_lo, s_hi) of one row (s = j * spp + k), each added as Li / spp,
+        into fb (a new zero framebuffer by default). A debugging aid (tools/rr_find.py)."""
+        if fb is None:
+            fb = np.zeros(p.width * p.height * 3, np.float32)
+        lib().tro_render_row_samples(self._h, ctypes.byref(p), fb.ctypes.data, row, s_lo, s_hi)
+        return fb
 
     def sample(self, p: Params, pixel: int, k: int):
         fb = np.zeros(p.width * p.height * 3, np.float32)

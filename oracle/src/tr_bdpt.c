@@ -1220,6 +1220,31 @@ int64_t tro_render(const tro_scene* s, const tro_params* p, float* fb, int row_b
     return n;
 }
 
+/* Debugging aid (tools/rr_find.py): samples [s_lo, s_hi) of one image row in the
+ * frame kernels' numbering (s = j * spp + k), each added as Li / spp on its own
+ * (the GPU's order of adds, not the reference's per-pixel sum). */
+int64_t tro_render_row_samples(const tro_scene* s, const tro_params* p, float* fb, int row, int64_t s_lo,
+                               int64_t s_hi) {
+    ctx_t c;
+    camdrv_t cd;
+    setup(&c, &cd, s, p, fb);
+    tr_sampler* smp = (tr_sampler*)malloc(sizeof(tr_sampler));
+    int64_t n = 0;
+    for (int64_t q = s_lo; q < s_hi; q++) {
+        const int j = (int)(q / p->spp), k = (int)(q % p->spp);
+        const int pixel = row * p->width + j;
+        mt_seed(smp, seed_for(p->seed_base, pixel, p->spp, k));
+        ray_t ray = camera_ray(&c, &cd, pixel, smp);
+        const v3 add = vscale(integrator_render(&c, ray, smp), 1.f / (float)p->spp);
+        fb[3 * (size_t)pixel + 0] += add.x;
+        fb[3 * (size_t)pixel + 1] += add.y;
+        fb[3 * (size_t)pixel + 2] += add.z;
+        n++;
+    }
+    free(smp);
+    return n;
+}
+
 void tro_sample(const tro_scene* s, const tro_params* p, int pixel, int k, float Li[3], float* fb) {
     ctx_t c;
     camdrv_t cd;
