@@ -366,6 +366,7 @@ __device__ BDPT_NOINLINE bool mt_ring_ahead(const LazyMT& r) {
     uint32_t* const ring = mt_ring_slot();
     uint32_t xa0 = ring[624], xa1 = ring[625], g = ring[626];
     const uint32_t want = r.n + BDPT_RING_AHEAD;
+    bool moved = false;  // the cursor changed: store it
     if (r.n < 227) {  // (x[n], x[n+1], x[n+397]) still in registers: the seed is recoverable
         const uint32_t seed = mt_seed_from(r.a0, r.n);
         // another seed's outputs, or this seed's past the window that still holds
@@ -381,12 +382,13 @@ __device__ BDPT_NOINLINE bool mt_ring_ahead(const LazyMT& r) {
             }
             xa0 = a0, xa1 = a1, g = 227;  // x[227], x[228]
             ring[627] = seed;
+            moved = true;
         }
     } else if (g < r.n) {
         return false;
     }
-    if (g >= want) return true;
     for (; g < want; g++) {
+        moved = true;
         uint32_t un, un1;
         if (g < 623) un = xa0, un1 = xa1;
         else if (g == 623) un = xa0, un1 = ring[0];
@@ -399,7 +401,9 @@ __device__ BDPT_NOINLINE bool mt_ring_ahead(const LazyMT& r) {
             xa0 = xa1;
         }
     }
-    ring[624] = xa0, ring[625] = xa1, ring[626] = g;
+    // (also after outputs 0..226 alone: a cursor left from the slot's previous seed
+    // next to this seed's ring[627] would read as this seed's outputs)
+    if (moved) ring[624] = xa0, ring[625] = xa1, ring[626] = g;
     return true;
 }
 __device__ __forceinline__ uint32_t mt_u32_long(LazyMT& r) {
