@@ -291,7 +291,7 @@ def main() -> None:
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    kernel_ms, reduce_ms, tail_ms, capped, parked = [], [], [], [], []
+    kernel_ms, reduce_ms, tail_ms, capped, parked, longs, express = [], [], [], [], [], [], []
 
     row_offset, row_stride = bdpt_dist.row_shard(rank, world)
 
@@ -303,7 +303,9 @@ def main() -> None:
         tail_ms.append(st.get("tail_ms", 0.0))
         capped.append(st.get("capped_samples", 0))
         parked.append(st.get("parked_samples", 0))
-        if st.get("schedule_errors"):  # a lane-decoupled task without its record, or draws past the generated ring
+        longs.append(st.get("rr_long_walks_max", 0))
+        express.append(st.get("rr_express_iters", [0, 0, 0]))
+        if st.get("schedule_errors"):  # draws past the generated MT19937 ring, or a continuation walk out of stack
             raise RuntimeError(f"{st['schedule_errors']} schedule errors in the render")
         if args.integrator == "path":
             integ.check_levels()  # a sample past the 512-level stack would not be the reference's
@@ -320,6 +322,8 @@ def main() -> None:
     tail_ms.clear()
     capped.clear()
     parked.clear()
+    longs.clear()
+    express.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -458,6 +462,10 @@ def main() -> None:
             out["config"]["russian_roulette"] = "NO_RR = 0 (bdpt.h:18)"
             out["russian_roulette"] = {"capped_samples_per_step": capped, "counting_pass_spp": cnt_cfg.spp,
                                        "parked_walks_per_step": parked,
+                                       # walks deeper than 512 bounces one wave held at once (max), and the
+                                       # express-mode loop iterations of waves holding 1 / 2..4 / more of them
+                                       "long_walks_per_wave_max_per_step": longs,
+                                       "express_iters_1_2to4_more_per_step": express,
                                        "continuation": "walks past BDPT_PARK_DEPTH bounces finished by the chain kernel "
                                                        "(one wave per walk) and resume launches",
                                        "max_light_depth": cst.get("max_light_depth"),

@@ -110,7 +110,7 @@ class _MultiStats(ctypes.Structure):  # bdpt_multi_stats
     _fields_ = [("devices", ctypes.c_int32), ("rccl", ctypes.c_int32), ("wall_ms", ctypes.c_double),
                 ("render_ms", ctypes.c_double), ("reduce_ms", ctypes.c_double), ("samples", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double * MAX_DEVICES), ("device_samples", ctypes.c_int64 * MAX_DEVICES),
-                ("capped_samples", ctypes.c_int64)]
+                ("capped_samples", ctypes.c_int64), ("schedule_errors", ctypes.c_int64)]
 
 
 class _MaterialDesc(ctypes.Structure):  # bdpt_material_desc
@@ -171,12 +171,13 @@ class _Stats(ctypes.Structure):
                 ("capped_samples", ctypes.c_int64), ("span_ms", ctypes.c_double), ("tail_ms", ctypes.c_double),
                 ("max_light_depth", ctypes.c_int64), ("max_eye_depth", ctypes.c_int64),
                 ("max_queries", ctypes.c_int64), ("schedule_errors", ctypes.c_int64), ("sched", ctypes.c_int64 * 4),
-                ("parked_samples", ctypes.c_int64)]
+                ("parked_samples", ctypes.c_int64), ("rr_long_walks_max", ctypes.c_int64),
+                ("rr_express_iters", ctypes.c_int64 * 3)]
 
 
 # Sources that make up the frame kernels' code objects: their hash stamps the
 # profiles (PMC passes) so bench.py only reuses a measurement of the same kernel.
-KERNEL_SOURCES = ("csrc/bdpt_kernels.hip", "csrc/bdpt_kernels_split.hip", "csrc/bdpt_kernels_dq.hip", "csrc/bdpt_path.hpp", "csrc/bdpt_device.hpp", "csrc/device_math.hpp",
+KERNEL_SOURCES = ("csrc/bdpt_kernels.hip", "csrc/bdpt_kernels_split.hip", "csrc/bdpt_path.hpp", "csrc/bdpt_device.hpp", "csrc/device_math.hpp",
                   "csrc/bdpt_types.h", "Makefile")
 
 
@@ -723,7 +724,8 @@ class BDPTIntegrator:
                     counters=dict(zip(COUNTER_NAMES, list(s.counters))), capped_samples=s.capped_samples,
                     span_ms=s.span_ms, tail_ms=s.tail_ms, max_light_depth=s.max_light_depth,
                     max_eye_depth=s.max_eye_depth, max_queries=s.max_queries, schedule_errors=s.schedule_errors, parked_samples=s.parked_samples,
-                    sched=dict(zip(("task_clocks", "tasks_popped", "tasks_without_ray", "own_tasks"), list(s.sched))),
+                    rr_long_walks_max=s.rr_long_walks_max, rr_express_iters=list(s.rr_express_iters),
+                    sched=dict(zip(("step_tasks", "shade_steps", "steps_ge32", "steps_ge64"), list(s.sched))),
                     kernel=(lib().bdpt_last_kernel(self._h) or b"").decode())
 
     def synchronize(self) -> None:
@@ -856,7 +858,7 @@ class MultiDeviceRenderer:
         n = s.devices
         return dict(devices=n, rccl=bool(s.rccl), wall_ms=s.wall_ms, render_ms=s.render_ms, reduce_ms=s.reduce_ms,
                     samples=s.samples, kernel_ms=list(s.kernel_ms)[:n], device_samples=list(s.device_samples)[:n],
-                    capped_samples=s.capped_samples)
+                    capped_samples=s.capped_samples, schedule_errors=s.schedule_errors)
 
 
 def debug_math(fn: str, x: np.ndarray, y: np.ndarray | None = None, device: int = 0) -> np.ndarray:

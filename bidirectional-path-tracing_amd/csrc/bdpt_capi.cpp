@@ -64,13 +64,6 @@ hipError_t launch_frame_split(const dev::DevScene& sc, const dev::DevFrame& fr, 
                               uint2* gstack, uint32_t nslots, unsigned long long* work, unsigned long long* counters,
                               int grid, hipStream_t stream, void* dparams);
 int frame_kernel_blocks_per_cu_split(size_t dyn_lds);
-// bdpt_kernels_dq.hip: the lane-decoupled build (connection tasks run by other lanes)
-size_t frame_params_bytes_dq();
-hipError_t launch_frame_dq(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, float* evbuf,
-                           uint32_t ev_max, uint2* gstack, uint32_t nslots, unsigned long long* work,
-                           unsigned long long* counters, int grid, hipStream_t stream, void* dparams);
-int frame_kernel_blocks_per_cu_dq(size_t dyn_lds);
-int frame_kernel_lds_stack_dq();
 size_t pt_params_bytes();
 int pt_blocks_per_cu(size_t dyn_lds);
 hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int32_t settings[8], float* fb,
@@ -91,13 +84,30 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+// Debugging knobs that change what a render computes (BDPT_SAMPLE_RANGE: a part
+// of the frame; BDPT_GRAZE_CODES=0: the plain near-cull rule, not exact on smooth
+// meshes) are read only when BDPT_DEBUG_KNOBS=1 is set too (tools/rr_find.py, A/B
+// sweeps); set without it they are ignored with one warning on stderr.
+const char* debug_knob(const char* name) {
+    const char* v = std::getenv(name);
+    if (!v) return nullptr;
+    const char* on = std::getenv("BDPT_DEBUG_KNOBS");
+    if (on && *on == '1') return v;
+    static bool warned = false;
+    if (!warned) {
+        warned = true;
+        std::fprintf(stderr, "bdpt_amd: %s is a debugging knob, ignored without BDPT_DEBUG_KNOBS=1\n", name);
+    }
+    return nullptr;
+}
+
 #define HIP_TRY(expr)                                                                               \
     do {                                                                                            \
         hipError_t e_ = (expr);                                                                     \
         if (e_ != hipSuccess) return fail(BDPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int kCounterWords = BDPT_NUM_COUNTERS + 3 + 4;  // sums, the counting pass's 3 maxima (Counts::m), Counts::q
+constexpr int kCounterWords = BDPT_NUM_COUNTERS + 3 + 4;  // sums, the counting pass's 3 maxima (Counts::m), the task histogram (Counts::q)
 constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
 // Short subpaths run the BDPT_SPLIT_CONTINUE build (bdpt_kernels_split.hip): the
 // ST_DEFER step it removes is one loop slot of the ~(rrDepth + 1)^2 / 2 a sample
@@ -106,13 +116,6 @@ constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227
 // HardLight rrDepth 2 / 3 / 4 / 5: +12.5 / +4.4 / +1.2 / -0.2 %).
 // BDPT_SPLIT_MAX_RR overrides the threshold (0: never).
 constexpr int kSplitMaxRrDepth = 3;
-// The lane-decoupled build (bdpt_kernels_dq.hip) for frames without Russian
-// roulette, rrDepth <= 28 and the BSDF table in LDS; BDPT_DQ=1 / 0 forces it on / off.
-constexpr bool kDqDefault = false;
-static bool use_dq_build() {
-    const char* e = std::getenv("BDPT_DQ");
-    return e ? *e == '1' : kDqDefault;
-}
 static bool use_split_build(int rr_depth) {
     const char* e = std::getenv("BDPT_SPLIT_MAX_RR");  // read per render (tests force either build)
     return rr_depth <= (e ? std::atoi(e) : kSplitMaxRrDepth);
@@ -191,9 +194,6 @@ struct bdpt_ctx {
     int64_t scene_bytes = 0;
     int64_t ntri = 0;  // triangles (shade records)
     uint32_t lds_words_base = 0;  // dynamic LDS words without the emitter faces / CDFs
-    float* ev = nullptr;          // the decoupled build's eye-vertex records
-    size_t ev_floats = 0;
-    void* dq_dparams = nullptr;
     // work buffers
     unsigned long long* work = nullptr;      // work counter
     unsigned long long* counters = nullptr;  // kCounters
@@ -306,7 +306,7 @@ static uint32_t graze_code(const float* v0, const float* v1, const float* v2, co
 // (n0, mat) (n1, shape) (n2, prim) (v1) (v2), + (v0) in the wide layout, with the
 // triangle's graze code in bits 24..31 of the shape word (shape ids < 2^24).
 static std::vector<float4_t> device_shade(const DeviceLayout& L) {
-    const char* gz = std::getenv("BDPT_GRAZE_CODES");  // "0": every code 0 (the plain |cos| < 0.02 test; A/B only)
+    const char* gz = debug_knob("BDPT_GRAZE_CODES");  // "0": every code 0 (the plain |cos| < 0.02 test; A/B only)
     const bool codes = !(gz && *gz == '0');
     const size_t ntri = L.shade.size() / 5;
     std::vector<float4_t> out(kShadeStride * ntri, float4_t{0.f, 0.f, 0.f, 0.f});
@@ -502,7 +502,7 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
                     static_cast<void*>(c->gstack), static_cast<void*>(c->tmp_fb), static_cast<void*>(c->sample_out), c->dparams,
                     static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
                     static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state), static_cast<void*>(c->capped),
-                    static_cast<void*>(c->diag), static_cast<void*>(c->ev), c->dq_dparams,
+                    static_cast<void*>(c->diag),
                     static_cast<void*>(c->splat_list), static_cast<void*>(c->park)})
         if (p) (void)hipFree(p);
     if (c->last_use) (void)hipEventDestroy(c->last_use);
@@ -643,7 +643,6 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     HIP_TRY(hipMalloc(&c->capped, sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->capped, 0, sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&c->dparams, frame_params_bytes()));
-    HIP_TRY(hipMalloc(&c->dq_dparams, frame_params_bytes_dq()));
     // Persistent grid: exactly the resident blocks (no co-residency is assumed:
     // the work queue has no inter-block waits, extra blocks would just queue).
     const size_t dyn = 4 * static_cast<size_t>(c->sc.lds_words);
@@ -654,8 +653,7 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     // right children; 4-wide: the host-computed bound), the part beyond the
     // kernel's LDS entries in HBM.
     const int depth = std::max(s->host.max_depth + 2, L.wmax_stack + 1);
-    // (the builds keep different numbers of entries in LDS: size for the fewest)
-    const int lds_entries = std::min(frame_kernel_lds_stack(), frame_kernel_lds_stack_dq());
+    const int lds_entries = frame_kernel_lds_stack();
     c->sc.gdepth = static_cast<uint32_t>(std::max(1, depth - lds_entries));  // per slot (DevScene::gdepth)
     const size_t spill_mega = static_cast<size_t>(c->sc.gdepth) * c->nslots;
     HIP_TRY(hipMalloc(&c->gstack, sizeof(uint2) * std::max<size_t>(1, spill_mega)));
@@ -750,18 +748,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     if (hbm && (p->rr_depth > kLazyRrDepth || rr))
         return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 or Russian roulette with BSDF records in HBM (too many "
                                           "materials for the LDS table) is not built");
-    const bool dq = !rr && p->rr_depth <= kLazyRrDepth && !hbm && use_dq_build();
-    // the decoupled build keeps two record buffers per lane slot (light and eye vertices, the eye records 128 B)
-    if ((rc = ensure_lv(c, fr.lv_max, dq ? 2 * c->nslots : c->nslots))) return rc;
-    if (dq) {
-        const size_t evn = static_cast<size_t>(p->rr_depth) * 32 * 2 * c->nslots;
-        if (evn > c->ev_floats) {
-            if (c->ev) HIP_TRY(hipFree(c->ev));
-            c->ev = nullptr;
-            HIP_TRY(hipMalloc(&c->ev, evn * sizeof(float)));
-            c->ev_floats = evn;
-        }
-    }
+    if ((rc = ensure_lv(c, fr.lv_max, c->nslots))) return rc;
     dev::DevScene sc = c->sc;
     sc.node_slack = node_slack_needed(c, eye, 1);
     if (p->rr_depth > kLazyRrDepth || rr) {  // draws past 226: the lanes' MT19937 rings
@@ -773,11 +760,13 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     HIP_TRY(hipMemsetAsync(c->work, 0, sizeof(unsigned long long), st));
     // BDPT_SAMPLE_RANGE="lo,hi" (debugging aid, tools/rr_find.py): only the shard's
     // samples [lo, hi) — the work counter starts at lo and the frame ends at hi
-    if (const char* sr = std::getenv("BDPT_SAMPLE_RANGE")) {
+    uint64_t range_lo = 0;  // samples [range_lo, total_samples) are rendered
+    if (const char* sr = debug_knob("BDPT_SAMPLE_RANGE")) {
         unsigned long long lo = 0, hi = 0;
         if (std::sscanf(sr, "%llu,%llu", &lo, &hi) == 2 && lo <= hi) {
             fr.total_samples = std::min<uint64_t>(fr.total_samples, hi);
             c->work_init = std::min<unsigned long long>(lo, fr.total_samples);
+            range_lo = c->work_init;
             HIP_TRY(hipMemcpyAsync(c->work, &c->work_init, sizeof(unsigned long long), hipMemcpyHostToDevice, st));
         }
     }
@@ -827,21 +816,6 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
             HIP_TRY(launch_frame_hbm(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, c->grid, st,
                                      c->dparams));
             c->last_kernel = "bdpt_frame_kernel_hbm";
-        } else if (dq) {
-            // the build's static LDS leaves less room: the emitter faces stay in HBM
-            // when keeping them in LDS would cost a resident block
-            dev::DevScene sdq = sc;
-            int blocks = frame_kernel_blocks_per_cu_dq(4 * static_cast<size_t>(sdq.lds_words));
-            if (sdq.lds_etri_off != dev::kNoLds &&
-                frame_kernel_blocks_per_cu_dq(4 * static_cast<size_t>(c->lds_words_base)) > blocks) {
-                sdq.lds_etri_off = sdq.lds_ecdf_off = dev::kNoLds;
-                sdq.lds_words = c->lds_words_base;
-                blocks = frame_kernel_blocks_per_cu_dq(4 * static_cast<size_t>(sdq.lds_words));
-            }
-            const int grid = std::min(c->grid, c->cus * blocks);
-            HIP_TRY(launch_frame_dq(sdq, fr, fb, c->lv, c->ev, static_cast<uint32_t>(p->rr_depth), c->gstack, c->nslots,
-                                    c->work, c->counters, grid, st, c->dq_dparams));
-            c->last_kernel = "bdpt_frame_kernel_dq";
         } else if (use_split_build(p->rr_depth)) {  // never more resident blocks than the slots allocated
             const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_split(
                                                            4 * static_cast<size_t>(c->sc.lds_words)));
@@ -860,7 +834,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     c->pending_timing = true;
     c->diag_pending = true;
     c->stats = bdpt_stats{};
-    c->stats.samples = static_cast<int64_t>(fr.total_samples);
+    c->stats.samples = static_cast<int64_t>(fr.total_samples - range_lo);
     c->stats.launches = launches;
     return BDPT_OK;
 }
@@ -1183,6 +1157,8 @@ int bdpt_get_stats(bdpt_ctx* c, bdpt_stats* out) {
                 c->stats.tail_ms = static_cast<double>(d[dev::kDiagEnd] - d[dev::kDiagLastClaim]) * tick_ms;
             c->stats.schedule_errors = static_cast<int64_t>(d[dev::kDiagErrors]);
             c->stats.parked_samples = static_cast<int64_t>(d[dev::kDiagParked]);
+            c->stats.rr_long_walks_max = static_cast<int64_t>(d[dev::kDiagLongMax]);
+            for (int k = 0; k < 3; k++) c->stats.rr_express_iters[k] = static_cast<int64_t>(d[dev::kDiagExpress1 + k]);
         }
         c->pending_timing = false;
     }
@@ -1223,8 +1199,8 @@ int bdpt_render_host(bdpt_ctx* c, const bdpt_frame_params* p, float* fb_host) {
         if ((rc = bdpt_get_stats(c, &st))) return rc;
         if (st.schedule_errors)
             return fail(BDPT_ERR_HIP, std::to_string(st.schedule_errors) +
-                                          " schedule errors (a lane-decoupled connection task that named no record, "
-                                          "or MT19937 draws past the generated ring)");
+                                          " schedule errors (MT19937 draws past the generated ring, or a continuation walk "
+                                          "out of stack)");
         if (p->russian_roulette && st.capped_samples)
             return fail(BDPT_ERR_UNSUPPORTED, std::to_string(st.capped_samples) +
                                                   " samples met the Russian-roulette bounds (light-vertex store / "

@@ -352,7 +352,9 @@ __device__ __forceinline__ uint32_t mt_seed_from(uint32_t x, uint32_t i) {
 // far fewer than BDPT_RING_AHEAD numbers (the action DAG's draw sites sum to
 // < 20). Per lane slot kMtRingWords words: the 624-word ring, then the
 // generator's cursor (x[g], x[g+1] of the seeding sequence while g < 623, g,
-// the seed whose outputs the ring holds).
+// the seed whose outputs the ring holds, and that seed's x[227] — the value a
+// lane's LazyMT::a0 keeps from draw 227 on, so a lane past 227 checks on every
+// call that the ring is its own).
 constexpr uint32_t kMtRingWords = kMtRingSlotWords;
 // The lane's slot: header word 3 (the block's first slot; the Russian-roulette
 // chain kernel stores the slot of the sample it continues there) + threadIdx.x.
@@ -382,9 +384,12 @@ __device__ BDPT_NOINLINE bool mt_ring_ahead(const LazyMT& r) {
             }
             xa0 = a0, xa1 = a1, g = 227;  // x[227], x[228]
             ring[627] = seed;
+            ring[628] = a0;  // x[227]: the ring's tag for lanes past draw 227
             moved = true;
         }
-    } else if (g < r.n) {
+    } else if (ring[628] != r.a0 || g < r.n) {
+        // another sample's ring (a stale cursor or tag), or this lane drew past
+        // what was generated: a schedule error the caller reports
         return false;
     }
     for (; g < want; g++) {
@@ -801,9 +806,18 @@ __device__ __forceinline__ float cull_far(float best) { return best + fabsf(best
 struct Counts {
     uint32_t c[kCounters];
     uint32_t m[3];  // maxima (counting pass): light-subpath depth, eye-subpath depth, queries per sample
-    uint32_t q[4];  // lane-decoupled build: task-phase wave clocks, ring tasks popped, tasks without a ray, own tasks
+    // connection-task histogram of the shading steps (frame kernels' counting pass): the
+    // tasks a wave holds when it shades — connectVertices still to run (nl - ci at A_CONN),
+    // connectToLight + all connections of a new eye vertex, connectToCamera of a new light
+    // vertex — summed over steps, the steps, steps with >= 32 and >= 64 tasks
+    uint32_t q[4];
+    uint32_t t_step;  // this lane's tasks in the current shading step
 };
-enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagErrors = 3, kDiagParked = 4, kDiagWords = 5 };
+// [5..8] Russian-roulette build: the most walks past BDPT_EXPRESS_DEPTH bounces one wave
+// held at once, and the express-mode loop iterations of waves holding 1, 2..BDPT_COOP_MAX,
+// more such walks
+enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagErrors = 3, kDiagParked = 4, kDiagLongMax = 5,
+             kDiagExpress1 = 6, kDiagExpressCoop = 7, kDiagExpressMore = 8, kDiagWords = 9 };
 
 // SIMD-efficiency probe: true on the lowest active lane of the wave only.
 __device__ __forceinline__ bool first_active_lane() {

@@ -72,6 +72,12 @@ constexpr int kBlock = 256;
 #ifndef BDPT_COOP_ALONE
 #define BDPT_COOP_ALONE (BDPT_RR == 1 && !BDPT_SAMPLER_STATE)  // a lone trapped walk walked by its whole wave (below)
 #endif
+#ifndef BDPT_COOP_MAX
+#define BDPT_COOP_MAX 4  // express waves with up to this many busy lanes walk their closest hits in turn with the whole wave
+#endif
+#ifndef BDPT_RR_DIAG
+#define BDPT_RR_DIAG 1
+#endif
 #ifndef BDPT_COOP_BATCH
 #define BDPT_COOP_BATCH 0  // the megakernel's wave walk tests leaves with wleaf_tests (coop_leaf's batched loads cost spills)
 #endif
@@ -299,6 +305,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     for (int i = 0; i < kCounters; i++) cnt.c[i] = 0;
     cnt.m[0] = cnt.m[1] = cnt.m[2] = 0;
     cnt.q[0] = cnt.q[1] = cnt.q[2] = cnt.q[3] = 0;
+    cnt.t_step = 0;
 #if BDPT_TID_REMAT
     LightStore ls = light_store(kp.lv, kp.fr.lv_max, blockIdx.x * kBlock);
     ls.tid_rel = true;
@@ -350,7 +357,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     // shading step (the frame cannot end before it does).
     bool long_walk = false;
 #if BDPT_COOP_ALONE
-    float coop_guess = -1.f;  // wave-uniform: the last hit distance of the wave's lone trapped walk
+    bool coop_wait = false;  // a closest-hit walk begun, waiting for its turn to be walked by the whole wave
 #endif
     const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
 #ifndef BDPT_DIAG
@@ -367,7 +374,15 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         uint64_t pa = (uint64_t)(ConstKParams)kpp;
         asm volatile("" : "+s"(pa));
         const KParams* P = (const KParams*)(ConstKParams)pa;
-        const bool express = BDPT_RR == 1 && BDPT_EXPRESS_DEPTH > 0 && __ballot(long_walk) != 0;  // wave-uniform
+        const uint64_t longs = BDPT_RR == 1 && BDPT_EXPRESS_DEPTH > 0 ? __ballot(long_walk) : 0ull;
+        const bool express = longs != 0;  // wave-uniform
+#if BDPT_RR == 1
+        if (BDPT_DIAG && BDPT_RR_DIAG && express && lane0() && P->fr.diag) {  // how many trapped walks share a wave (bdpt_stats)
+            const int k = __popcll(longs);
+            gmax(P->fr.diag + kDiagLongMax, static_cast<unsigned long long>(k));
+            gadd(P->fr.diag + (k == 1 ? kDiagExpress1 : k <= BDPT_COOP_MAX ? kDiagExpressCoop : kDiagExpressMore), 1ull);
+        }
+#endif
 #if BDPT_SEED_CHUNK
         // Refill idle lanes from the wave's chunk of 64 consecutive samples. A
         // chunk is claimed with one atomic and the seeding recurrence of all its
@@ -466,12 +481,19 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             L.c.depth > P->fr.park_depth && park_lane(P->fr, P->nslots, blockIdx.x * kBlock + opaque_tid(), L)) {
             L.state = ST_PARKED;
             long_walk = false;
+#if BDPT_COOP_ALONE
+            coop_wait = false;
+#endif
         }
 #endif
 #if BDPT_COOP_ALONE
         bool began = false;  // this lane began a culled closest-hit walk in this iteration
 #endif
+#if BDPT_COOP_ALONE
+        if (BDPT_BUSY(L.state) && !tracing && !has_res && !coop_wait) {  // a new query: begin its walk
+#else
         if (BDPT_BUSY(L.state) && !tracing && !has_res) {  // a new query: begin its walk
+#endif
             q_any = is_shadow_state(L.state);
             if (COUNT && L.state != ST_DEFER) cnt.c[q_any ? 1 : 0]++;
             ri = ray_inv(L.ray, cull_near_for(L));
@@ -497,20 +519,31 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     res = -1, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;  // no child hit: a miss
                     tracing = false;
                     has_res = true;
+#if BDPT_COOP_ALONE
+                    began = false;  // (complete: nothing for the wave to walk)
+#endif
                 }
 #endif
             }
         }
 #if BDPT_COOP_ALONE
-        // A subpath trapped in glass alone in its wave (express mode): the wave walks
-        // its closest hit together (coop_closest: ~10 rounds instead of ~30 steps)
-        // on the LDS stack columns of its lanes; bounded by twice the last hit
-        // first (a chain in glass repeats its chord lengths). If the columns do
-        // not suffice, the lane walks alone from the root.
+        // Subpaths trapped in glass (express mode: the wave no longer refills). When
+        // the wave holds at most BDPT_COOP_MAX busy lanes and each of them has a
+        // closest-hit walk begun (in this iteration, or waiting from an earlier one),
+        // the wave walks one of them with all 64 lanes (coop_closest: ~10 rounds
+        // instead of ~30 dependent steps) on the LDS stack columns of its lanes — no
+        // lane holds a walk in progress then, so the columns are free — and the
+        // others wait for their turn (waiting lanes first, so every walk gets one).
+        // The walk is bounded by twice the lane's last hit distance first (a chain in
+        // glass repeats its chord lengths). A lane whose walk did not fit the columns
+        // walks alone from the root; waiting lanes walk alone once the wave holds more
+        // than BDPT_COOP_MAX busy lanes or leaves express mode (their walk restarts),
+        // in their turn: a walk begun while another lane still walks alone waits too.
         if (!COUNT && express) {
-            const uint64_t busy = __ballot(BDPT_BUSY(L.state));
-            if (__popcll(busy) == 1 && __ballot(began) == busy) {
-                const int b = __ffsll(static_cast<unsigned long long>(busy)) - 1;
+            const uint64_t busy = __ballot(BDPT_BUSY(L.state)), wt = __ballot(coop_wait), bg = __ballot(began);
+            if (__popcll(busy) <= BDPT_COOP_MAX && (bg | wt) == busy) {
+                const int b = __ffsll(static_cast<unsigned long long>(wt ? wt : bg)) - 1;
+                const int me = static_cast<int>(opaque_tid() & 63);
                 Ray q;
                 q.o = mk(__shfl(L.ray.o.x, b), __shfl(L.ray.o.y, b), __shfl(L.ray.o.z, b));
                 q.d = mk(__shfl(L.ray.d.x, b), __shfl(L.ray.d.y, b), __shfl(L.ray.d.z, b));
@@ -519,17 +552,19 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 qi.inv = mk(__shfl(ri.inv.x, b), __shfl(ri.inv.y, b), __shfl(ri.inv.z, b));
                 qi.near = __shfl(ri.near, b);
                 qi.fast = true;
+                // the lane's last hit distance (Hit::dist, shade_hit), the bound's guess
+                const float guess = BDPT_GRAZE_IN_DIST ? -1.f : __shfl(L.h.dist, b);
                 const CoopStack cs{stack_mem + (threadIdx.x & ~63u), kBlock};
                 float t = 0.f, u = 0.f, v = 0.f;
                 int r = -1;
                 bool ok = true;
-                for (int pass = coop_guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
-                    const float bound = pass == 0 ? 2.f * coop_guess : q.max_t;
+                for (int pass = guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
+                    const float bound = pass == 0 ? 2.f * guess : q.max_t;
                     ok = SLACK ? coop_closest<true, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v)
                                : coop_closest<false, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v);
                 }
-                coop_guess = ok && r >= 0 ? t : -1.f;
-                if (began) {
+                if (me == b) {
+                    coop_wait = false;
                     if (ok) {
                         res = r, rt = t, ru = u, rv = v;
                         tracing = false;
@@ -537,8 +572,22 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     } else {
                         ts = trav_begin(tsc, L.ray);  // its stack columns were the wave's
                     }
+                } else if (began) {
+                    coop_wait = true;  // its turn comes in a later iteration
+                    tracing = false;
                 }
+            } else if (__popcll(busy) <= BDPT_COOP_MAX) {
+                // some lane still walks alone (a shadow ray, or a walk that did not fit
+                // the columns): walks begun now wait for it, so they are walked by the wave
+                if (began) {
+                    coop_wait = true;
+                    tracing = false;
+                }
+            } else {
+                coop_wait = false;  // too many busy lanes: waiting walks restart alone next iteration
             }
+        } else {
+            coop_wait = false;
         }
 #endif
         const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
@@ -574,6 +623,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             }
         }
         const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+        const bool shading = COUNT && __ballot(has_res) != 0;
         if (has_res) {
             has_res = false;
 #if BDPT_DEEP_RNG && BDPT_RING_AHEAD
@@ -591,6 +641,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const uint64_t c2 = __builtin_amdgcn_s_memtime();
             cnt.c[12] += static_cast<uint32_t>(c1 - c0);
             cnt.c[13] += static_cast<uint32_t>(c2 - c1);
+        }
+        if (COUNT && shading) {  // the connection tasks the wave held in this shading step (Counts::q)
+            uint32_t tw = cnt.t_step;
+            for (int off = 32; off > 0; off >>= 1) tw += static_cast<uint32_t>(__shfl_xor(static_cast<int>(tw), off));
+            cnt.t_step = 0;
+            if (lane0()) cnt.q[0] += tw, cnt.q[1]++, cnt.q[2] += tw >= 32u, cnt.q[3] += tw >= 64u;
         }
 #else
         if (L.state != ST_IDLE) step<FULL, COUNT>(L, P->sc, P->fr, P->fb, ls, stk, cnt);

@@ -276,6 +276,7 @@ int bdpt_multi_render_host(bdpt_multi* m, const bdpt_frame_params* params, const
     m->stats.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
     m->stats.samples = 0;
     m->stats.capped_samples = 0;
+    m->stats.schedule_errors = 0;
     for (int i = 0; i < N; i++) {
         bdpt_stats s;
         if ((rc = bdpt_get_stats(m->ctx[i], &s))) return rc;
@@ -283,7 +284,14 @@ int bdpt_multi_render_host(bdpt_multi* m, const bdpt_frame_params* params, const
         m->stats.device_samples[i] = s.samples;
         m->stats.samples += s.samples;
         m->stats.capped_samples += s.capped_samples;
+        m->stats.schedule_errors += s.schedule_errors;
     }
+    // as bdpt_render_host: MT19937 draws past the generated ring (or a continuation
+    // walk out of stack) on any device mean the frame was rendered from wrong numbers
+    if (m->stats.schedule_errors)
+        return bdpt::set_error(BDPT_ERR_HIP, std::to_string(m->stats.schedule_errors) +
+                                                 " schedule errors over the devices (MT19937 draws past the "
+                                                 "generated ring, or a continuation walk out of stack)");
     // as bdpt_render_host: a Russian-roulette frame in which some sample met the
     // light-vertex store or the bounce guard is not the reference's image
     if (params->russian_roulette && !path && !direct && m->stats.capped_samples)

@@ -417,6 +417,7 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
         if (rr_on(fr)) L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);  /* bdpt.h:201-204 */ \
         const BsdfRecord& b = bsdf_of(sc, L.h.mat); \
         if (is_delta(b)) break; \
+        if (COUNT) cnt.t_step++;  /* a camera-connection task (Counts::q) */ \
         /* connectToCamera (bdpt.h:295-371): everything but the visibility test. */ \
         f3 e2l = L.h.p - cam_o; \
         const float invD2 = rcp_cr(dot(e2l, e2l)); \
@@ -503,6 +504,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                         const LightStore& ls, Counts& cnt) {
     const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
     const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
+    if (COUNT && act == A_CONN && fr.strategy == 0) cnt.t_step += static_cast<uint32_t>(L.c.nl - L.c.ci);  // (Counts::q)
 #if BDPT_SPLIT_CONTINUE
     BDPT_BODY_LIGHT_VERTEX
     BDPT_BODY_CONTINUE(A_LIGHT_CONTINUE, act == A_LIGHT_CONTINUE)
@@ -620,6 +622,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
     } BDPT_END;
     BDPT_ACTION(25, act == A_NEE) {  // connectToLight (bdpt.h:374-430): everything but the visibility test
         act = A_CONN;
+        if (COUNT) cnt.t_step += 1u + (fr.strategy == 0 ? static_cast<uint32_t>(L.c.nl) : 0u);  // (Counts::q)
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         const EmitterRecord& e = emitter_of(sc, e_id);
         f3 dir = L.h.p - e_p;

@@ -147,14 +147,19 @@ typedef struct {
     int64_t max_light_depth; /* counting pass (BDPT_FLAG_COUNT) maxima over the samples: light-subpath */
     int64_t max_eye_depth;   /* depth, eye-subpath depth, */
     int64_t max_queries;     /* ray queries of one sample */
-    int64_t schedule_errors; /* connection tasks of the lane-decoupled build whose descriptor named no record,
-                                MT19937 draws past the generated ring, a continuation walk out of stack
+    int64_t schedule_errors; /* MT19937 draws past the generated ring (or a ring left by another sample), a
+                                continuation walk out of stack
                                 (any non-zero count is a bug, and bdpt_render_host fails) */
-    int64_t sched[4];        /* counting pass of the lane-decoupled build: task-phase wave clocks, tasks
-                                popped from the block rings, tasks that traced no shadow ray, tasks their
-                                owner ran itself (ring full) */
+    int64_t sched[4];        /* counting pass (BDPT_FLAG_COUNT), the connection tasks a wave holds when it
+                                shades (connectVertices still to run, connectToLight + the connections of a
+                                new eye vertex, connectToCamera of a new light vertex): summed over the
+                                shading steps, the shading steps, steps with >= 32 and with >= 64 tasks */
     int64_t parked_samples;  /* Russian roulette: walks handed to the continuation pass's chain kernel
                                 (deeper than BDPT_PARK_DEPTH bounces; a sample may be handed over again) */
+    int64_t rr_long_walks_max;  /* Russian roulette: the most subpaths deeper than 512 bounces one wave held
+                                   at once (such a wave stops refilling: express mode) */
+    int64_t rr_express_iters[3]; /* Russian roulette: loop iterations of express-mode waves holding 1, 2..4,
+                                    more than 4 such subpaths (up to 4 are walked in turn by the whole wave) */
 } bdpt_stats;
 
 const char* bdpt_last_error(void);
@@ -370,6 +375,8 @@ typedef struct {
     int64_t device_samples[BDPT_MAX_DEVICES];
     int64_t capped_samples;  /* Russian roulette: bdpt_stats.capped_samples summed over the devices; a
                                 non-zero sum fails bdpt_multi_render_host as it fails bdpt_render_host */
+    int64_t schedule_errors; /* bdpt_stats.schedule_errors summed over the devices; a non-zero sum fails
+                                bdpt_multi_render_host (BDPT_ERR_HIP) as it fails bdpt_render_host */
 } bdpt_multi_stats;
 int bdpt_multi_create(const bdpt_scene* scene, int32_t ndevices, const int32_t* devices, bdpt_multi** out);
 int bdpt_multi_destroy(bdpt_multi* multi);

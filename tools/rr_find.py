@@ -41,6 +41,7 @@ stream = torch.cuda.current_stream().cuda_stream
 
 def gpu_row(row, rng=None):
     if rng:
+        os.environ["BDPT_DEBUG_KNOBS"] = "1"
         os.environ["BDPT_SAMPLE_RANGE"] = f"{rng[0]},{rng[1]}"
     fb.zero_()
     it.render_device(fb.data_ptr(), stream, row_offset=row, row_stride=H)

@@ -49,9 +49,13 @@ for flags, label in passes:
     out = {"pass": label, "scene": name, "W": W, "H": H, "spp": spp, "rows": [off, stride], "samples": st["samples"],
            "kernel_ms": round(st["kernel_ms"], 3), "span_ms": round(st["span_ms"], 3),
            "tail_ms": round(st["tail_ms"], 3), "capped": st["capped_samples"],
-           "parked": st.get("parked_samples"), "launches": st.get("launches"), "sched": st.get("sched"), "wall_s": round(time.time() - t, 3),
+           "parked": st.get("parked_samples"), "launches": st.get("launches"),
+           "long_walks_max": st.get("rr_long_walks_max"), "express_iters_1_2to4_more": st.get("rr_express_iters"),
+           "wall_s": round(time.time() - t, 3),
            "kernel": st["kernel"]}
     if flags:
         out.update(max_light_depth=st["max_light_depth"], max_eye_depth=st["max_eye_depth"],
-                   max_queries=st["max_queries"], counters=st["counters"])
+                   max_queries=st["max_queries"], counters=st["counters"],
+                   trav_simd_eff=round(st["counters"]["trav_lane_iters"] / max(64 * st["counters"]["trav_wave_iters"], 1), 4),
+                   shade_simd_eff=round(st["counters"]["shade_lane_actions"] / max(64 * st["counters"]["shade_wave_actions"], 1), 4))
     print(json.dumps(out), flush=True)
