@@ -1747,7 +1747,7 @@ __device__ __forceinline__ int sample_emitter(const DevScene& sc, Rng& rng, floa
     const float w = 1 - uv.x - uv.y;
     pos = (v0 * w + v1 * uv.x) + v2 * uv.y;
     n = normalize((n0 * w + n1 * uv.x) + n2 * uv.y);
-    pos_pdf = rcp_cr(e.area);
+    pos_pdf = rcp_w(e.area);
     if (graze) *graze = __float_as_int(g.z) << 24;  // the face's graze code (bdpt_capi.cpp device_emit_tri)
     return static_cast<int>(id);
 }

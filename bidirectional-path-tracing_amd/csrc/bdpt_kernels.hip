@@ -28,6 +28,17 @@
 #endif
 #endif
 
+// The frame kernels without Russian roulette weight paths with the hardware
+// reciprocal / square root (device_math.hpp rcp_w): the paths stay the
+// reference's bit for bit, contributions move by a few ulp. The Russian-roulette
+// build (its throughput steers the roulette) and the single-sample build keep the
+// IEEE operations.
+#ifndef BDPT_FAST_WEIGHTS
+#if !(defined(BDPT_SAMPLER_STATE) && BDPT_SAMPLER_STATE) && !(defined(BDPT_RR) && BDPT_RR)
+#define BDPT_FAST_WEIGHTS 1
+#endif
+#endif
+
 // The eye-estimate slots (bdpt_path.hpp) are claimed with the 64-sample chunks.
 #if defined(BDPT_SEED_CHUNK) && !BDPT_SEED_CHUNK && !defined(BDPT_EYE_SLOTS)
 #define BDPT_EYE_SLOTS 0

@@ -128,15 +128,15 @@ __device__ __forceinline__ bool continue_walk(const BsdfRecord& b, const Hit& h,
     pdf *= rrp;
     const float absCosOut = fabsf(wi.z);
     if (is_zero(f)) return false;
-    tp = tp * (f * rcp_cr(pdf));
+    tp = tp * (f * rcp_w(pdf));
     depth++;
     const float prevRev = delta ? pdf : bsdf_pdf(b, h.wo, wi) * rrp;  // pdf of the swapped (wo, wi)
     if (delta) {
-        vc = div_cr(absCosOut, pdf) * (prevRev * vc);
+        vc = div_w(absCosOut, pdf) * (prevRev * vc);
         vcm = 0.f;
     } else {
-        vc = div_cr(absCosOut, pdf) * (vcm + prevRev * vc);
-        vcm = rcp_cr(pdf);
+        vc = div_w(absCosOut, pdf) * (vcm + prevRev * vc);
+        vcm = rcp_w(pdf);
     }
     ray = Ray{h.p, world_at(h.n, wi), kEpsilon, 3.402823466e+38f};  // FLT_MAX (core.h:120)
     return true;
@@ -411,8 +411,8 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
         const float dist2 = L.h.dist * L.h.dist; \
         BDPT_DIST_TO_GRAZE \
         const float absCosIn = fabsf(L.h.wo.z); \
-        L.c.vcm *= div_cr(dist2, absCosIn); \
-        L.c.vc *= rcp_cr(absCosIn); \
+        L.c.vcm *= div_w(dist2, absCosIn); \
+        L.c.vc *= rcp_w(absCosIn); \
         act = A_LIGHT_CONTINUE; \
         if (rr_on(fr)) L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);  /* bdpt.h:201-204 */ \
         const BsdfRecord& b = bsdf_of(sc, L.h.mat); \
@@ -420,8 +420,8 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
         if (COUNT) cnt.t_step++;  /* a camera-connection task (Counts::q) */ \
         /* connectToCamera (bdpt.h:295-371): everything but the visibility test. */ \
         f3 e2l = L.h.p - cam_o; \
-        const float invD2 = rcp_cr(dot(e2l, e2l)); \
-        e2l = e2l * sqrt_cr(invD2); \
+        const float invD2 = rcp_w(dot(e2l, e2l)); \
+        e2l = e2l * sqrt_w(invD2); \
         int xp, yp; \
         splat_pixel(fr.cam, L.h.p, xp, yp); \
         if (xp < 0 || yp < 0 || xp >= fr.W || yp >= fr.H) break; \
@@ -433,19 +433,19 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
         const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo); \
         const f3 f = ep.f; \
         if (is_zero(f) || (!early_cos_ && wi.z <= 0.f)) break; \
-        const float d = div_cr(fr.cam.vnear, cosCamera); \
-        const float img2solid = div_cr(d * d, cosCamera); \
+        const float d = div_w(fr.cam.vnear, cosCamera); \
+        const float img2solid = div_w(d * d, cosCamera); \
         const float img2surf = img2solid * (wi.z * invD2); \
-        const float surf2img = rcp_cr(img2surf); \
+        const float surf2img = rcp_w(img2surf); \
         const float nlight = static_cast<float>(fr.W * fr.H); \
-        f3 rad = L.c.tp * (f * rcp_cr(wi.z)); \
-        rad = rad * rcp_cr(surf2img); \
+        f3 rad = L.c.tp * (f * rcp_w(wi.z)); \
+        rad = rad * rcp_w(surf2img); \
         rad = rad * fr.inv_pixels;  /* rcp(nlight) */ \
         rad = rad * fr.inv_spp;  /* rcp(spp) */ \
         const float reversePdf_a = 1.f * img2surf; \
         const float prevRev = ep.rev * (rr_on(fr) ? L.c.rr : 1.f);  /* swapped (wi, wo) * lightVertex.rr (bdpt.h:342) */ \
-        const float lightWeight = div_cr(reversePdf_a, nlight) * (L.c.vcm + prevRev * L.c.vc); \
-        const float mis = rcp_cr(lightWeight + 1.f + 0.f); \
+        const float lightWeight = div_w(reversePdf_a, nlight) * (L.c.vcm + prevRev * L.c.vc); \
+        const float mis = rcp_w(lightWeight + 1.f + 0.f); \
         L.c.pend = (fr.strategy == 0) ? rad * mis : rad; \
         L.c.pend_px = yp * fr.W + xp; \
         L.ray = shadow_ray(cam_o, L.h.p); \
@@ -520,11 +520,11 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             break;
         }
         const float cosCamera = dot(fwd, L.c.cam_d);
-        const float d = div_cr(fr.cam.vnear, cosCamera);
-        const float t1Pdf = 1.f * div_cr(d * d, cosCamera);
+        const float d = div_w(fr.cam.vnear, cosCamera);
+        const float t1Pdf = 1.f * div_w(d * d, cosCamera);
         L.c.tp = mk(1.f, 1.f, 1.f);
         L.c.vc = 0.f;
-        L.c.vcm = static_cast<float>(fr.W * fr.H) * rcp_cr(t1Pdf);
+        L.c.vcm = static_cast<float>(fr.W * fr.H) * rcp_w(t1Pdf);
         L.c.depth = 1;
         L.c.pure = 1u;
         if (rr_on(fr)) L.c.rr = 1.f;  // rrProbability before the first vertex (bdpt.h:65)
@@ -544,8 +544,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const float dist2 = L.h.dist * L.h.dist;
         BDPT_DIST_TO_GRAZE
         const float absCosIn = fabsf(L.h.wo.z);
-        L.c.vcm *= div_cr(dist2, absCosIn);
-        L.c.vc *= rcp_cr(absCosIn);
+        L.c.vcm *= div_w(dist2, absCosIn);
+        L.c.vc *= rcp_w(absCosIn);
         const BsdfRecord& b = bsdf_of(sc, L.h.mat);
         const f3 emission = ld3(b.emission);  // getEmission = materials[matID].emission
         if (!is_zero(emission)) {
@@ -555,9 +555,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
                 const float emitterPdf = sc.inv_nemit;  // 1.f / nemit
                 if (L.c.depth > 1) {
                     f3 contrib = ld3(e.radiance) * L.c.tp;
-                    const float pA = rcp_cr(e.area * emitterPdf);
+                    const float pA = rcp_w(e.area * emitterPdf);
                     const float camW = pA * L.c.vcm + (pA * kInvTwoPi) * L.c.vc;
-                    const float mis = rcp_cr(1.f + camW);
+                    const float mis = rcp_w(1.f + camW);
                     if (fr.strategy == 2) {  // PATH_TRACING (bdpt.h:110-113)
                         if (L.c.pure) L.c.Li = L.c.Li + contrib;
                     } else {
@@ -604,9 +604,9 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
 #endif
         if (BDPT_EMIT_GRAZE) L.h.shape = e_graze;  // its graze code (the shape id is not read before the walk's resolve)
         if (BDPT_GRAZE_IN_DIST) L.h.dist = graze_threshold(e_graze);
-        L.c.tp = (ld3(e.radiance) * edir.z) * rcp_cr(emissionPdf);
-        L.c.vc = edir.z * rcp_cr(emissionPdf);
-        L.c.vcm = div_cr(areaPdf, emissionPdf);
+        L.c.tp = (ld3(e.radiance) * edir.z) * rcp_w(emissionPdf);
+        L.c.vc = edir.z * rcp_w(emissionPdf);
+        L.c.vcm = div_w(areaPdf, emissionPdf);
         L.c.nl = 0;
         L.c.depth = 1;
         if (rr_on(fr)) L.c.rr = 1.f;  // bdpt.h:187
@@ -627,7 +627,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const EmitterRecord& e = emitter_of(sc, e_id);
         f3 dir = L.h.p - e_p;
         const float d2 = dot(dir, dir);
-        dir = dir * rcp_cr(sqrt_cr(d2));
+        dir = dir * rsqrt_w(d2);
 #if BDPT_CONN_EARLY_COS >= 2
         const float cosAtLight = dot(e_n, dir);
         const float cosAtEye = dot(-dir, L.h.n);  // = the frame's z component (to_local)
@@ -639,16 +639,16 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const float cosAtEye = wi.z;
         if (cosAtLight <= 0.f || cosAtEye <= 0.f) break;
 #endif
-        const float pdf_w = div_cr((e_pdf * e_pos_pdf) * d2, cosAtLight);
+        const float pdf_w = div_w((e_pdf * e_pos_pdf) * d2, cosAtLight);
         const EvalPdfs ep = bsdf_eval_pdfs(b, wi, L.h.wo);
-        const f3 Li = ((ep.f * rcp_cr(pdf_w)) * L.c.tp) * ld3(e.radiance);
+        const f3 Li = ((ep.f * rcp_w(pdf_w)) * L.c.tp) * ld3(e.radiance);
         if (is_zero(Li)) break;
         const float rrE = rr_on(fr) ? L.c.rr : 1.f;  // eyeVertex.rr (bdpt.h:410, :417)
-        const float lightWeight = div_cr(ep.fwd * rrE, pdf_w);
+        const float lightWeight = div_w(ep.fwd * rrE, pdf_w);
         const float eyePrevRev = ep.rev * rrE;
-        const float eyeCurRev_a = cosAtEye * rcp_cr(d2) * kInvTwoPi;
+        const float eyeCurRev_a = cosAtEye * rcp_w(d2) * kInvTwoPi;
         const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
-        const float mis = rcp_cr(lightWeight + 1.f + eyeWeight);
+        const float mis = rcp_w(lightWeight + 1.f + eyeWeight);
         L.c.pend = (fr.strategy == 0) ? Li * mis : Li;
         L.ray = shadow_ray(L.h.p, e_p);
         L.state = ST_NEE;
@@ -665,8 +665,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             const Vertex V = load_vertex(ls, L.c.ci);
             if (COUNT) cnt.c[5]++;
             f3 dir = L.h.p - V.p;
-            const float invD2 = rcp_cr(dot(dir, dir));
-            dir = dir * sqrt_cr(invD2);
+            const float invD2 = rcp_w(dot(dir, dir));
+            dir = dir * sqrt_w(invD2);
 #if BDPT_CONN_EARLY_COS >= 1
             // the frames' z components are dot(v, n) (to_local), so the
             // rejection test runs before the frames are built
@@ -700,7 +700,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             const float eyePathRev_a = eyePathRev_w * cosE * invD2;
             const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
             const float eyeWeight = eyePathRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
-            const float mis = rcp_cr(lightWeight + 1.f + eyeWeight);
+            const float mis = rcp_w(lightWeight + 1.f + eyeWeight);
             L.c.pend = Li * mis;
             L.ray = shadow_ray(L.h.p, V.p);
             L.state = ST_CONN;

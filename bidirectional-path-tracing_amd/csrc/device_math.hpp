@@ -108,6 +108,25 @@ __device__ __forceinline__ float div_cr(float a, float b) {
     return a / b;
 }
 __device__ __forceinline__ f3 normalize(f3 v) { return v * rcp_cr(sqrt_cr(dot(v, v))); }
+
+// Arithmetic that only WEIGHTS a path — the MIS recursion (vc, vcm), pdf ratios,
+// throughput and contributions — and never steers it (no direction, hit, pixel or
+// random-number decision depends on it; a cosine sign computed from a direction
+// normalized this way flips only where the connection's contribution is 0). With
+// BDPT_FAST_WEIGHTS these take the hardware's 1-ulp v_rcp_f32 / v_sqrt_f32 /
+// v_rsq_f32 instead of the correctly rounded ~11-instruction sequences: every
+// sample still follows the reference's path bit for bit, its contributions differ
+// by a few ulp (per-pixel ~1e-6 relative, against the 1e-4 bound). The frame
+// kernels without Russian roulette build with it (bdpt_kernels.hip); the Russian-
+// roulette build (whose throughput steers the roulette) and the single-sample and
+// per-function kernels keep the IEEE operations.
+#ifndef BDPT_FAST_WEIGHTS
+#define BDPT_FAST_WEIGHTS 0
+#endif
+__device__ __forceinline__ float rcp_w(float x) { return BDPT_FAST_WEIGHTS ? __builtin_amdgcn_rcpf(x) : rcp_cr(x); }
+__device__ __forceinline__ float div_w(float a, float b) { return BDPT_FAST_WEIGHTS ? a * __builtin_amdgcn_rcpf(b) : div_cr(a, b); }
+__device__ __forceinline__ float sqrt_w(float x) { return BDPT_FAST_WEIGHTS ? __builtin_amdgcn_sqrtf(x) : sqrt_cr(x); }
+__device__ __forceinline__ float rsqrt_w(float x) { return BDPT_FAST_WEIGHTS ? __builtin_amdgcn_rsqf(x) : rcp_cr(sqrt_cr(x)); }
 __device__ __forceinline__ bool is_zero(f3 v) { return v.x == 0.f && v.y == 0.f && v.z == 0.f; }
 __device__ __forceinline__ f3 xyz(float4 q) { return mk(q.x, q.y, q.z); }
 
