@@ -274,6 +274,64 @@ uint32_t collapse(const std::vector<BNode>& bn, const std::function<uint32_t(con
     return root;
 }
 
+// Node order in memory. The collapse emits nodes depth-first (a node's first
+// child follows it; its siblings come after that child's whole subtree).
+// BDPT_NODE_ORDER=bfs lays the tree out level by level; =treelet in treelets of
+// kTreeletDepth levels (1 + 4 + 16 nodes, contiguous, breadth-first inside), each
+// followed by the treelets below it in child order — the order a walk's next few
+// levels are read in. Links are renumbered; node 0 stays the root.
+constexpr int kTreeletDepth = 3;
+void reorder_nodes(WideBvh& out) {
+    const char* mode = std::getenv("BDPT_NODE_ORDER");
+    if (!mode || std::string(mode) == "dfs") return;
+    const bool bfs = std::string(mode) == "bfs";
+    const size_t nn = out.nodes.size() / 8;
+    if (nn < 2) return;
+    auto kids = [&](uint32_t i, uint32_t (&l)[kWideArity]) {
+        std::memcpy(l, &out.nodes[8 * static_cast<size_t>(i) + 6], sizeof(l));
+    };
+    std::vector<uint32_t> order;
+    order.reserve(nn);
+    if (bfs) {
+        order.push_back(0);
+        for (size_t h = 0; h < order.size(); h++) {
+            uint32_t l[kWideArity];
+            kids(order[h], l);
+            for (uint32_t c : l)
+                if (c != kEmptyLink && !(c & kLeafBit)) order.push_back(c);
+        }
+    } else {
+        std::function<void(uint32_t)> treelet = [&](uint32_t root) {
+            std::vector<uint32_t> level{root}, frontier;
+            for (int d = 0; d < kTreeletDepth && !level.empty(); d++) {
+                std::vector<uint32_t> next;
+                for (uint32_t i : level) {
+                    order.push_back(i);
+                    uint32_t l[kWideArity];
+                    kids(i, l);
+                    for (uint32_t c : l)
+                        if (c != kEmptyLink && !(c & kLeafBit)) (d + 1 < kTreeletDepth ? next : frontier).push_back(c);
+                }
+                level.swap(next);
+            }
+            for (uint32_t f : frontier) treelet(f);
+        };
+        treelet(0);
+    }
+    std::vector<uint32_t> newid(nn, kEmptyLink);
+    for (size_t k = 0; k < order.size(); k++) newid[order[k]] = static_cast<uint32_t>(k);
+    std::vector<float4_t> nodes(out.nodes.size());
+    for (size_t k = 0; k < order.size(); k++) {
+        std::memcpy(&nodes[8 * k], &out.nodes[8 * static_cast<size_t>(order[k])], 8 * sizeof(float4_t));
+        uint32_t l[kWideArity];
+        std::memcpy(l, &nodes[8 * k + 6], sizeof(l));
+        for (uint32_t& c : l)
+            if (c != kEmptyLink && !(c & kLeafBit)) c = newid[c];
+        std::memcpy(&nodes[8 * k + 6], l, sizeof(l));
+    }
+    out.nodes.swap(nodes);
+}
+
 }  // namespace
 
 bool build_wide_bvh(const std::vector<FlatNode>& flat, WideBvh& out, std::string& err) {
@@ -406,6 +464,7 @@ bool build_wide_bvh_tris(const std::vector<FlatNode>& flat, const std::vector<fl
         return make_leaf_link(static_cast<uint32_t>(c.leaf), static_cast<uint32_t>(c.count));
     }, out.bvh);
     out.bvh.leaves = wleaves;
+    reorder_nodes(out.bvh);
     if (out.bvh.root_link != 0) {
         err = "wide BVH root must be node 0";
         return false;
