@@ -237,6 +237,9 @@ def main() -> None:
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--rr-depth", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--count-spp", type=int, default=None,
+                    help="spp of the untimed counting pass (default min(spp, 16); 1 with --russian-roulette, where "
+                         "a trapped subpath's chain runs at the lone lane's pace in that pass)")
     ap.add_argument("--russian-roulette", action="store_true",
                     help="the reference's NO_RR = 0 branch (bdpt.h:18, :68, :129-132, :188, :201-204): subpaths "
                          "continue past rrDepth by roulette; the bdpt_frame_kernel_rr build, checked against "
@@ -375,9 +378,12 @@ def main() -> None:
         print(json.dumps(out), flush=True)
     elif rank == 0:
         # algorithmic bytes per sample from a counting pass (untimed, same seeds, smaller spp)
-        # (Russian roulette: 1 spp — the counting pass keeps every walk in the megakernel,
-        # so a trapped subpath's chain there runs at the lone lane's pace)
-        cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=1 if args.russian_roulette else min(spp, 16),
+        # (Russian roulette: 1 spp by default — the counting pass keeps every walk in the
+        # megakernel, so a trapped subpath's chain there runs at the lone lane's pace; at 1 spp
+        # every lane holds one sample, so its SIMD-efficiency counters measure a frame that is
+        # all drain: --count-spp 16 for scenes without trapped subpaths)
+        count_spp = args.count_spp or (1 if args.russian_roulette else min(spp, 16))
+        cnt_cfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=count_spp,
                                   rr_depth=rr,
                                   russian_roulette=rrm)
         cnt = bdpt_amd.BDPTIntegrator(integ.scene, cnt_cfg, device=gpu if world > 1 else 0)
@@ -471,6 +477,9 @@ def main() -> None:
                                        "max_light_depth": cst.get("max_light_depth"),
                                        "max_eye_depth": cst.get("max_eye_depth"),
                                        "max_queries_per_sample": cst.get("max_queries"),
+                                       # SIMD efficiency of the counting pass (lane iterations / 64 x wave iterations)
+                                       "trav_simd_eff": round(cts["trav_lane_iters"] / max(64 * cts["trav_wave_iters"], 1), 4),
+                                       "shade_simd_eff": round(cts["shade_lane_actions"] / max(64 * cts["shade_wave_actions"], 1), 4),
                                        "tail_ms": roof["tail_ms"], "kernel": cst.get("kernel")}
         if ranks:
             out["ranks"] = ranks

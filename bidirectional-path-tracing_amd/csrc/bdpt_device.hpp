@@ -819,6 +819,11 @@ struct Counts {
 enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagErrors = 3, kDiagParked = 4, kDiagLongMax = 5,
              kDiagExpress1 = 6, kDiagExpressCoop = 7, kDiagExpressMore = 8, kDiagWords = 9 };
 
+// Set bits of a wave mask as an int. (HIP's __popcll is typed unsigned long long
+// here: mixed with int in min / max it selected the double overloads, and the
+// refill and shade-threshold arithmetic ran in f64.)
+__device__ __forceinline__ int popc64(uint64_t m) { return __builtin_popcountll(m); }
+
 // SIMD-efficiency probe: true on the lowest active lane of the wave only.
 __device__ __forceinline__ bool first_active_lane() {
     return (__lane_id()) == static_cast<unsigned>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1);
@@ -1385,7 +1390,7 @@ __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, 
             const uint64_t has = __ballot(lnk[c] != kEmptyLinkDev);
             const int pos = sp + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
                                      static_cast<uint32_t>(has >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(has), 0u)));
-            const int n = __popcll(has);
+            const int n = popc64(has);
             if (sp + n > cap) {
                 ok = false;
             } else if (lnk[c] != kEmptyLinkDev) {

@@ -389,7 +389,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         const bool express = longs != 0;  // wave-uniform
 #if BDPT_RR == 1
         if (BDPT_DIAG && BDPT_RR_DIAG && express && lane0() && P->fr.diag) {  // how many trapped walks share a wave (bdpt_stats)
-            const int k = __popcll(longs);
+            const int k = popc64(longs);
             gmax(P->fr.diag + kDiagLongMax, static_cast<unsigned long long>(k));
             gadd(P->fr.diag + (k == 1 ? kDiagExpress1 : k <= BDPT_COOP_MAX ? kDiagExpressCoop : kDiagExpressMore), 1ull);
         }
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 chunk_seq++;
 #endif
             }
-            const int m = min(__popcll(idle), chunk_n - chunk_pos);
+            const int m = min(popc64(idle), chunk_n - chunk_pos);
             const int rank = lanes_below(idle);
             const uint32_t x397 = __shfl(chunk_x397, (chunk_pos + rank) & 63);
             if (L.state == ST_IDLE && rank < m) start_sample<true>(L, chunk_base + chunk_pos + rank, P->fr, x397);
@@ -453,7 +453,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         if (!exhausted) {  // refill idle lanes: one atomic per wave
             const uint64_t idle = __ballot(L.state == ST_IDLE);
             if (idle) {
-                const int n = __popcll(idle);
+                const int n = popc64(idle);
                 const int leader = __ffsll(static_cast<unsigned long long>(idle)) - 1;
                 unsigned long long base = 0;
                 if ((opaque_tid() & 63) == static_cast<uint32_t>(leader)) base = gadd(work, static_cast<unsigned long long>(n));
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // while the slow walkers resume afterwards from where they stopped.
 #if BDPT_RR == 1 && BDPT_EXPRESS_WALK
         if (!COUNT && express) {  // a trapped subpath alone in its wave: its delta chain out of line
-            const bool alone = __popcll(__ballot(BDPT_BUSY(L.state))) == 1;
+            const bool alone = popc64(__ballot(BDPT_BUSY(L.state))) == 1;
             if (alone && !tracing && !has_res && (L.state == ST_LIGHT || L.state == ST_EYE)) {
                 if (express_walk(L, P->sc, P->fr, P->fb, stk, res, rt, ru, rv)) has_res = true;
                 if (!has_res) {
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // in their turn: a walk begun while another lane still walks alone waits too.
         if (!COUNT && express) {
             const uint64_t busy = __ballot(BDPT_BUSY(L.state)), wt = __ballot(coop_wait), bg = __ballot(began);
-            if (__popcll(busy) <= BDPT_COOP_MAX && (bg | wt) == busy) {
+            if (popc64(busy) <= BDPT_COOP_MAX && (bg | wt) == busy) {
                 const int b = __ffsll(static_cast<unsigned long long>(wt ? wt : bg)) - 1;
                 const int me = static_cast<int>(opaque_tid() & 63);
                 Ray q;
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     coop_wait = true;  // its turn comes in a later iteration
                     tracing = false;
                 }
-            } else if (__popcll(busy) <= BDPT_COOP_MAX) {
+            } else if (popc64(busy) <= BDPT_COOP_MAX) {
                 // some lane still walks alone (a shadow ray, or a walk that did not fit
                 // the columns): walks begun now wait for it, so they are walked by the wave
                 if (began) {
@@ -606,9 +606,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const uint64_t tr = __ballot(tracing);
             if (!tr) break;
             const uint64_t ready = __ballot(has_res);
-            if (__popcll(ready) >= (express ? 1
+            if (popc64(ready) >= (express ? 1
                                     : BDPT_TAIL_SHADE == 1 && exhausted ? 1
-                                    : BDPT_TAIL_SHADE == 2 && exhausted ? max(1, (__popcll(tr | ready) * BDPT_TAIL_FRAC) >> 3)
+                                    : BDPT_TAIL_SHADE == 2 && exhausted ? max(1, (popc64(tr | ready) * BDPT_TAIL_FRAC) >> 3)
                                                                         : BDPT_SHADE_READY))
                 break;
 #if BDPT_TRAV_SPLIT
@@ -617,7 +617,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             // below) instead of both code paths running in every iteration.
             const bool at_leaf = (ts.link & kLeafBit) != 0;
             const uint64_t lv = __ballot(tracing && at_leaf);
-            const bool do_leaf = __popcll(lv) * 4 >= __popcll(tr & ~lv) * BDPT_TRAV_SPLIT;
+            const bool do_leaf = popc64(lv) * 4 >= popc64(tr & ~lv) * BDPT_TRAV_SPLIT;
             bool fin = tracing && at_leaf == do_leaf && trav_step<COUNT, SLACK>(tsc, L.ray, ri, q_any, ts, stk, cnt);
             // BDPT_WALK_UNROLL more interior-node steps before the wave's ballots
 #pragma unroll

@@ -668,13 +668,13 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
         if (!exhausted) {  // refill idle lanes: one atomic per wave
             const uint64_t idle = __ballot(!L.busy);
             if (idle) {
-                const int n = __popcll(idle);
+                const int n = popc64(idle);
                 const int leader = __ffsll(static_cast<unsigned long long>(idle)) - 1;
                 unsigned long long base = 0;
                 if (lane == leader) base = gadd(P.work, static_cast<unsigned long long>(n));
                 base = __shfl(base, leader);
                 if (!L.busy) {
-                    const uint64_t s = base + __popcll(idle & ((1ull << lane) - 1ull));
+                    const uint64_t s = base + popc64(idle & ((1ull << lane) - 1ull));
                     if (s < total) {
                         L.rng.seed = sample_seed(s, P.fr, L.pixel);
                         mt_seed(L.rng.m, L.rng.seed);
@@ -722,10 +722,10 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
         for (;;) {
             const uint64_t tr = __ballot(tracing);
             if (!tr) break;
-            if (__popcll(__ballot(has_res)) >= PT_SHADE_READY) break;
+            if (popc64(__ballot(has_res)) >= PT_SHADE_READY) break;
             const bool at_leaf = (ts.link & kLeafBit) != 0;
             const uint64_t lv = __ballot(tracing && at_leaf);
-            const bool do_leaf = __popcll(lv) * 4 >= __popcll(tr & ~lv) * PT_TRAV_SPLIT;
+            const bool do_leaf = popc64(lv) * 4 >= popc64(tr & ~lv) * PT_TRAV_SPLIT;
             if (tracing && at_leaf == do_leaf && trav_step<COUNT>(tsc, L.ray, ri, false, ts, stk, cnt)) {
                 res = ts.best, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;
                 tracing = false;
