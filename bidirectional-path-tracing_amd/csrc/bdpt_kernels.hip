@@ -56,7 +56,7 @@ constexpr int kBlock = 256;
 #define BDPT_OVERLAP 1  // overlapped walk / shade schedule in the megakernel (0: one query then shade, in lockstep)
 #endif
 #ifndef BDPT_TRAV_SPLIT
-#define BDPT_TRAV_SPLIT 8  // > 0: leaf and interior-node steps in separate iterations (leaf step if 4 * leaf lanes >= SPLIT * node lanes)
+#define BDPT_TRAV_SPLIT 6  // > 0: leaf and interior-node steps in separate iterations (leaf step if 4 * leaf lanes >= SPLIT * node lanes; round 5 re-sweep: 6 over 8)
 #endif
 #ifndef BDPT_SEED_CHUNK
 #define BDPT_SEED_CHUNK 1  // refill from per-wave chunks of 64 samples seeded together (0: per-refill seeding)
@@ -65,7 +65,7 @@ constexpr int kBlock = 256;
 #define BDPT_WALK_UNROLL 1  // extra interior-node steps per walk iteration (measured: 0: 201.7, 1: 203.6)
 #endif
 #ifndef BDPT_SHADE_READY
-#define BDPT_SHADE_READY 48  // lanes with a finished query that trigger the wave's shading step
+#define BDPT_SHADE_READY 44  // lanes with a finished query that trigger the wave's shading step (round 5 re-sweep: 44 over 48)
 #endif
 #ifndef BDPT_TAIL_SHADE
 #define BDPT_TAIL_SHADE 2  // once a wave has no samples left to claim: 1 shade at 1 ready lane, 2 at BDPT_TAIL_FRAC / 8 of its busy lanes
