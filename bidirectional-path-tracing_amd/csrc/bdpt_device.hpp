@@ -509,7 +509,7 @@ __device__ __forceinline__ f3 phong_lobe(F2 u, float ex) {
     return mk(sinTheta * sc.c, sinTheta * sc.s, cosTheta);
 }
 __device__ __forceinline__ float phong_lobe_pdf(f3 v, float ex) {
-    return v.z >= 0.f ? (ex + 2) * kInvTwoPi * glibc_powf(v.z, ex) : 0.f;
+    return v.z >= 0.f ? (ex + 2) * kInvTwoPi * pow_w(v.z, ex) : 0.f;
 }
 // squareToUniformTriangle (math.h:229-234)
 __device__ __forceinline__ F2 uniform_triangle(F2 s) {
@@ -1452,7 +1452,7 @@ __device__ __forceinline__ f3 glossy_eval(const BsdfRecord& b, f3 wi, f3 wo) {
         if (b.ks[0] != 0.f || b.ks[1] != 0.f || b.ks[2] != 0.f) {
             const float ex = b.exponent;
             const float c = glibc_fminf(glibc_fmaxf(dot(wi, reflect_z(wo)), 0.f), 1.f);
-            val = val + ((ld3(b.ks) * (ex + 2)) * kInvTwoPi) * glibc_powf(c, ex);
+            val = val + ((ld3(b.ks) * (ex + 2)) * kInvTwoPi) * pow_w(c, ex);
         }
         val = val * b.scale;
         val = val * wi.z;
@@ -1529,7 +1529,7 @@ __device__ __forceinline__ EvalPdfs bsdf_eval_pdfs(const BsdfRecord& b, f3 wi, f
     const bool lobe_pdf = kind == BSDF_PHONG || b.specw != 0.f;
     float pw = 0.f;
     if ((eval_on && ks_on) || (lobe_pdf && z >= 0.f))
-        pw = glibc_powf(z > 1.f ? z : glibc_fminf(glibc_fmaxf(z, 0.f), 1.f), ex);
+        pw = pow_w(z > 1.f ? z : glibc_fminf(glibc_fmaxf(z, 0.f), 1.f), ex);
     if (eval_on) {  // glossy_eval
         f3 val = mk(0.f, 0.f, 0.f);
         val = val + ld3(b.kd) * kInvPi;

@@ -93,8 +93,12 @@ __device__ __forceinline__ float4 lv_ld(const float4* p) {
     return gld4(p);
 #endif
 }
+#ifndef BDPT_PROBE_NO_LV_STORE
+#define BDPT_PROBE_NO_LV_STORE 0  // accounting probe only (a wrong image): light-vertex records not written
+#endif
 __device__ __forceinline__ void store_vertex(const LightStore& ls, int v, const Hit& h, f3 tp, float vcm, float vc,
                                              float rr) {
+    if (BDPT_PROBE_NO_LV_STORE) return;
     float4* q = ls.at(v);
     lv_st(q, make_float4(h.p.x, h.p.y, h.p.z, vcm));
     lv_st(q + 1, make_float4(h.n.x, h.n.y, h.n.z, vc));
@@ -254,6 +258,9 @@ struct Lane {
 // The single-sample build returns the splats of its one sample as a list
 // instead (fb = header {count, capacity, 0, 0} then (pixel, r, g, b) records),
 // so the caller adds them to its own framebuffer in the reference's order.
+#ifndef BDPT_PROBE_NO_SPLAT
+#define BDPT_PROBE_NO_SPLAT 0
+#endif
 __device__ __forceinline__ void splat_add(float* __restrict__ fb, int pixel, f3 v) {
 #if BDPT_SAMPLER_STATE
     uint32_t* const hdr = reinterpret_cast<uint32_t*>(fb);
@@ -263,6 +270,8 @@ __device__ __forceinline__ void splat_add(float* __restrict__ fb, int pixel, f3 
         float* e = fb + 4 + 4 * static_cast<size_t>(k);
         e[0] = __int_as_float(pixel), e[1] = v.x, e[2] = v.y, e[3] = v.z;
     }
+#elif BDPT_PROBE_NO_SPLAT
+    (void)fb, (void)pixel, (void)v;  // accounting probe only (a wrong image): no camera-splat atomics
 #else
     float* px = fb + 3 * static_cast<size_t>(pixel);
     gadd(px + 0, v.x);

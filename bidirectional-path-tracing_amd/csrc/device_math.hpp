@@ -419,5 +419,21 @@ __device__ BDPT_POWF_ATTR float glibc_powf(float x, float y) {
     return powf_exp2(ylogx, sign_bias);
 }
 
+// x^y for a Phong lobe's value or pdf (weights only, see rcp_w): with
+// BDPT_FAST_WEIGHTS exp2(y * log2(x)) on the hardware's v_log_f32 / v_exp_f32,
+// else glibc's powf. The callers pass x in [0, 1] (or just above 1 by rounding)
+// and y = the exponent >= 0; the relative error y * |log2 x| * ~2^-22 is largest
+// where x^y is tiny. y == 0 gives 1 as powf does (also for x == 0).
+#ifndef BDPT_FAST_POW
+#define BDPT_FAST_POW BDPT_FAST_WEIGHTS
+#endif
+__device__ __forceinline__ float pow_w(float x, float y) {
+#if BDPT_FAST_POW
+    return y == 0.f ? 1.f : __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+#else
+    return glibc_powf(x, y);
+#endif
+}
+
 }  // namespace dev
 }  // namespace bdpt
