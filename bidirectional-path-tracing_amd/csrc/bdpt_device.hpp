@@ -176,6 +176,9 @@ struct DevFrame {
     uint32_t* park;
     int32_t park_depth;
     uint32_t park_flags;
+    // lanes with a finished query that trigger a wave's shading step (the frame
+    // kernels; chosen per render by the host: 0 = the build's BDPT_SHADE_READY)
+    int32_t shade_ready;
 };
 enum : uint32_t { kParkOn = 1u, kParkResume = 2u };
 

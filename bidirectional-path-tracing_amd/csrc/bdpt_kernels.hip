@@ -609,7 +609,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             if (popc64(ready) >= (express ? 1
                                     : BDPT_TAIL_SHADE == 1 && exhausted ? 1
                                     : BDPT_TAIL_SHADE == 2 && exhausted ? max(1, (popc64(tr | ready) * BDPT_TAIL_FRAC) >> 3)
-                                                                        : BDPT_SHADE_READY))
+                                                                        : (P->fr.shade_ready > 0 ? P->fr.shade_ready : BDPT_SHADE_READY)))
                 break;
 #if BDPT_TRAV_SPLIT
             // Lanes at a leaf and lanes at an interior node step in alternate
