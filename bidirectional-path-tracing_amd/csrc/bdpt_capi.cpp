@@ -718,17 +718,29 @@ static int ensure_lv(bdpt_ctx* c, int lv_max, uint32_t nslots) {
 // the camera is within 100 diagonals of the scene the plain tn <= tf test is
 // conservative and the ambiguity slack is skipped. Other rays
 // (bdpt_intersect's, the refleaf tree's unpadded boxes) keep it.
+//
+// BDPT_SLAB_FMA builds test those boxes by one fma per plane (slab_fma), whose
+// error also grows with the origin's distance from 0 (2^-24 |o_i| per plane in
+// scene units): they skip the slack only while the origins and the scene box
+// also lie within kFmaCoordDiags diagonals of 0, where the per-plane error,
+// 2^-23 · 101 + 2^-24 · 300 < 3e-5 diagonals, stays below slab_fast's own bound
+// at 100 diagonals (3.6e-7 · 202 = 7.3e-5) and far inside the padding.
+constexpr double kFmaCoordDiags = 300.0;
 static uint32_t node_slack_needed(const bdpt_ctx* c, const float* const* origins, int n) {
     if (!c->tri_tree) return 1u;
     double diag2 = 0.0;
     for (int a = 0; a < 3; a++) diag2 += (c->box_hi[a] - c->box_lo[a]) * (c->box_hi[a] - c->box_lo[a]);
     if (!(diag2 > 0.0) || !std::isfinite(diag2)) return 1u;
+    const double coord_max = BDPT_SLAB_FMA ? kFmaCoordDiags * std::sqrt(diag2) : HUGE_VAL;
+    for (int a = 0; a < 3; a++)
+        if (!(std::fabs(c->box_lo[a]) <= coord_max && std::fabs(c->box_hi[a]) <= coord_max)) return 1u;
     for (int k = 0; k < n; k++) {
         double far2 = 0.0;  // squared distance to the farthest corner of the scene box
         for (int a = 0; a < 3; a++) {
             const double o = origins[k][a];
             const double d = std::max(std::fabs(o - c->box_lo[a]), std::fabs(o - c->box_hi[a]));
             far2 += d * d;
+            if (!(std::fabs(o) <= coord_max)) return 1u;
         }
         if (!std::isfinite(far2) || far2 > 1.0e4 * diag2) return 1u;
     }

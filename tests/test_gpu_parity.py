@@ -105,6 +105,33 @@ def test_gpu_far_camera_takes_the_slack_test_and_matches_oracle(name, dist):
     assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
 
 
+# coordinates ~250 diagonals from 0: the slack-free interior test (by one fma per
+# plane in the BDPT_SLAB_FMA builds); ~350: past kFmaCoordDiags, the slack test (bdpt_capi.cpp)
+# (HardLight's 0.08-unit light keeps its area only up to ~100 diagonals: float
+# coordinates near 800 flatten its faces, and the loader then finds no emitter)
+@pytest.mark.parametrize("name,diags", [("caustic", 250.0), ("caustic", 350.0), ("hardlight", 100.0)])
+def test_gpu_translated_scene_matches_oracle(name, diags, tmp_path):
+    """The scene and camera moved far from the origin along (1, 1, 1): both sides
+    of the host's coordinate-magnitude condition on the slack-free interior test
+    render the oracle's frame."""
+    with open(variants.obj_path(name)) as f:
+        v = np.array([line.split()[1:4] for line in f if line.startswith("v ")], np.float64)
+    off = np.full(3, diags * np.linalg.norm(v.max(0) - v.min(0)))  # |coordinate| ~ diags diagonals per axis
+    path = variants.translated_obj(name, str(tmp_path), off)
+    cam = dict(variants.SCENES[name]["camera"])
+    cam["eye"] = [float(np.float32(e + o)) for e, o in zip(cam["eye"], off)]
+    cam["at"] = [float(np.float32(a + o)) for a, o in zip(cam["at"], off)]
+    W, H, spp, rr = 32, 32, 4, variants.SCENES[name]["rr_depth"]
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**cam), width=W, height=H, spp=spp, rr_depth=rr)
+    it = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(path), cfg)
+    it.init()
+    fb = it.render_frame().reshape(-1)
+    ref, _ = O.Scene(path).render(O.make_params(cam, W, H, spp, rr))
+    assert (ref.reshape(-1, 3).sum(1) > 0).mean() > 0.2  # the box is in view
+    worst, exact, _ = report(fb, ref)
+    assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
+
+
 @pytest.mark.parametrize("name,W,H,spp,rr", [
     ("caustic", 24, 40, 3, 1),    # rrDepth 1: both walks stop at once (2 draws)
     ("caustic", 24, 40, 3, 2),
