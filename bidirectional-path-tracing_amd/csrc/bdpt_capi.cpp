@@ -191,6 +191,7 @@ struct bdpt_ctx {
     dev::DevScene sc{};
     int max_depth = 0;
     bool tri_tree = false;              // traversal boxes padded (wide_bvh.hpp kTriBoxPad)
+    int64_t wnode_bytes = 0;            // the 4-wide node array (BDPT_SLAB_SIGN: 32-bit offsets into it)
     double box_lo[3] = {}, box_hi[3] = {};  // scene bounds (the reference BVH's root box)
     int64_t scene_bytes = 0;
     int64_t ntri = 0;  // triangles (shade records)
@@ -577,6 +578,7 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     c->sc.root_link = L.root_link;
     c->sc.node_slack = 1u;  // per render: node_slack_needed
     c->tri_tree = L.tri_tree;
+    c->wnode_bytes = static_cast<int64_t>(L.wnodes.size()) * 16;
     for (int a = 0; a < 3; a++) c->box_lo[a] = s->host.nodes[0].bmin[a], c->box_hi[a] = s->host.nodes[0].bmax[a];
     {  // the region whose queries the culled, padded traversal tree serves (DevScene::near_lo/hi)
         double diag2 = 0.0;
@@ -731,7 +733,9 @@ static uint32_t node_slack_needed(const bdpt_ctx* c, const float* const* origins
     double diag2 = 0.0;
     for (int a = 0; a < 3; a++) diag2 += (c->box_hi[a] - c->box_lo[a]) * (c->box_hi[a] - c->box_lo[a]);
     if (!(diag2 > 0.0) || !std::isfinite(diag2)) return 1u;
-    const double coord_max = BDPT_SLAB_FMA ? kFmaCoordDiags * std::sqrt(diag2) : HUGE_VAL;
+    // BDPT_SLAB_SIGN builds address the node planes by 32-bit offsets (load_wnode_nf)
+    if (BDPT_SLAB_SIGN && c->wnode_bytes >= (int64_t{1} << 32)) return 1u;
+    const double coord_max = BDPT_SLAB_FMA || BDPT_SLAB_SIGN ? kFmaCoordDiags * std::sqrt(diag2) : HUGE_VAL;
     for (int a = 0; a < 3; a++)
         if (!(std::fabs(c->box_lo[a]) <= coord_max && std::fabs(c->box_hi[a]) <= coord_max)) return 1u;
     for (int k = 0; k < n; k++) {
