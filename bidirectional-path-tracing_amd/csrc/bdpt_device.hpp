@@ -836,7 +836,19 @@ struct LinkStack {
 // ALL reachable leaves, first-found (= lowest leaf index) on ties. Boxes
 // entered beyond best + margin, or exited before t = 5e-4, cannot hold a
 // triangle that changes that result.
-__device__ __forceinline__ float cull_far(float best) { return best + fabsf(best) * 1e-3f + 1e-4f; }
+#ifndef BDPT_CULL_FMA
+#define BDPT_CULL_FMA 1  // the margin's product and sum as one fma (the same bound within an ulp; the margin is 1e-3 relative)
+#endif
+__device__ __forceinline__ float cull_far(float best) {
+    return BDPT_CULL_FMA ? fmaf(fabsf(best), 1e-3f, best) + 1e-4f : best + fabsf(best) * 1e-3f + 1e-4f;
+}
+// The far bound of a walk in progress. An occlusion query's best_t stays its
+// max_t (trav_begin; wleaf_tests returns at its first hit without lowering it),
+// so ts.best_t serves both kinds of query.
+#ifndef BDPT_FAR_BEST
+#define BDPT_FAR_BEST 1  // 0: the select on the query kind (with CULL_FMA and ROOT_NF: Caustic +0.65 %, HardLight +0.65 %, synth1m +0.6 %)
+#endif
+#define BDPT_WALK_FAR(any, r, ts) cull_far(BDPT_FAR_BEST ? (ts).best_t : ((any) ? (r).max_t : (ts).best_t))
 
 struct Counts {
     uint32_t c[kCounters];
@@ -1085,7 +1097,7 @@ __device__ __forceinline__ bool trav_pop(const Ray& r, bool any, TravState& ts, 
                                          uint32_t* culled = nullptr) {
     while (ts.sp > 0) {
         const uint2 e = stk.get(--ts.sp);
-        if (!(__uint_as_float(e.y) > cull_far(any ? r.max_t : ts.best_t))) {
+        if (!(__uint_as_float(e.y) > BDPT_WALK_FAR(any, r, ts))) {
             ts.link = e.x;
             return true;
         }
@@ -1238,7 +1250,7 @@ __device__ __forceinline__ bool trav_node_vals(const WNode& n, const Ray& r, con
     if (COUNT) cnt.c[2]++;
     float key[4];
     uint32_t lnk[4];
-    node_child_keys<SLACK, NF>(n, r, ri, cull_far(any ? r.max_t : ts.best_t), key, lnk);
+    node_child_keys<SLACK, NF>(n, r, ri, BDPT_WALK_FAR(any, r, ts), key, lnk);
     if (lnk[0] == kEmptyLinkDev) return false;
     if (lnk[3] != kEmptyLinkDev) stk.put(ts.sp++, lnk[3], key[3]);
     if (lnk[2] != kEmptyLinkDev) stk.put(ts.sp++, lnk[2], key[2]);
@@ -1278,18 +1290,46 @@ __device__ __forceinline__ void root_lds_fill(RootLds& m, const DevScene& sc) {
 }
 // The root and (when the walk descends into an interior child) that child;
 // false when the query is already complete (a miss: nothing below was hit).
+#ifndef BDPT_ROOT_NF
+#define BDPT_ROOT_NF 1  // the LDS root and children through the sign-picked planes too (lds_wnode_nf)
+#endif
+#if !BDPT_QNODES && BDPT_SLAB_SIGN && BDPT_ROOT_NF
+// load_wnode_nf's plane vectors from an LDS copy of a node (the same 16-byte
+// vectors at the same offsets: the copy is the record's first 112 bytes)
+__device__ __forceinline__ WNode lds_wnode_nf(const WNode& m, f3 inv) {
+    const char* b = reinterpret_cast<const char*>(&m);
+    const uint32_t sx = plane_sel(inv.x), sy = plane_sel(inv.y), sz = plane_sel(inv.z);
+    WNode n;
+    n.v[0] = *reinterpret_cast<const float4*>(b + sx);
+    n.v[1] = *reinterpret_cast<const float4*>(b + (sx ^ 16u));
+    n.v[2] = *reinterpret_cast<const float4*>(b + 32 + sy);
+    n.v[3] = *reinterpret_cast<const float4*>(b + 32 + (sy ^ 16u));
+    n.v[4] = *reinterpret_cast<const float4*>(b + 64 + sz);
+    n.v[5] = *reinterpret_cast<const float4*>(b + 64 + (sz ^ 16u));
+    n.v[6] = m.v[6];
+    return n;
+}
+#endif
+template <bool COUNT, bool SLACK>
+__device__ __forceinline__ bool root_node_vals(const WNode& m, const Ray& r, const RayInv& ri, bool any, TravState& ts,
+                                               const Stack& stk, Counts& cnt) {
+#if !BDPT_QNODES && BDPT_SLAB_SIGN && BDPT_ROOT_NF
+    if (!SLACK) return trav_node_vals<COUNT, false, true>(lds_wnode_nf(m, ri.inv), r, ri, any, ts, stk, cnt);
+#endif
+    return trav_node_vals<COUNT, SLACK>(m, r, ri, any, ts, stk, cnt);
+}
 template <bool COUNT, bool SLACK>
 __device__ __forceinline__ bool walk_begin_lds(const RootLds& m, const Ray& r, const RayInv& ri, bool any,
                                                TravState& ts, const Stack& stk, Counts& cnt) {
     if (COUNT) cnt.c[8]++;
-    bool live = trav_node_vals<COUNT, SLACK>(m.root, r, ri, any, ts, stk, cnt);
+    bool live = root_node_vals<COUNT, SLACK>(m.root, r, ri, any, ts, stk, cnt);
     if (live && !(ts.link & kLeafBit)) {
         const float4 lk = m.root.v[kNodeLinks];
         const int k = ts.link == __float_as_uint(lk.x) ? 0
                       : ts.link == __float_as_uint(lk.y) ? 1
                       : ts.link == __float_as_uint(lk.z) ? 2 : 3;
         if (COUNT) cnt.c[8]++;
-        live = trav_node_vals<COUNT, SLACK>(m.kid[k], r, ri, any, ts, stk, cnt) || trav_pop(r, any, ts, stk);
+        live = root_node_vals<COUNT, SLACK>(m.kid[k], r, ri, any, ts, stk, cnt) || trav_pop(r, any, ts, stk);
     }
     return live;
 }
