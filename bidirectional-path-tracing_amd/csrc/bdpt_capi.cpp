@@ -899,6 +899,19 @@ static int ensure_pt(bdpt_ctx* c, int levels) {
     return BDPT_OK;
 }
 
+// The path tracer's and direct integrator's scene: its queries start inside the
+// scene box or at the camera, as the BDPT frame's do, so the same per-render
+// choice of interior-box test applies (node_slack_needed).
+#ifndef BDPT_PT_SLACK_FREE
+#define BDPT_PT_SLACK_FREE 1  // 0: the path tracer keeps the slack test everywhere (A/B only)
+#endif
+static dev::DevScene pt_scene(const bdpt_ctx* c, const bdpt_frame_params* p) {
+    dev::DevScene sc = c->sc;
+    const float* eye[1] = {p->camera.eye};
+    sc.node_slack = BDPT_PT_SLACK_FREE ? node_slack_needed(c, eye, 1) : 1u;
+    return sc;
+}
+
 int bdpt_render_path(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_params* path, float* fb,
                      void* hip_stream) {
     if (!c || !fb || !path) return fail(BDPT_ERR_INVALID, "null argument");
@@ -925,7 +938,7 @@ int bdpt_render_path(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_path_pa
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kCounterWords, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
     if (fr.total_samples > 0)
-        HIP_TRY(launch_pt(c->sc, fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
+        HIP_TRY(launch_pt(pt_scene(c, p), fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
                           c->counters, c->pt_grid, st, c->pt_dparams));
     HIP_TRY(hipEventRecord(c->ev1, st));
     if ((rc = end_use(c, st))) return rc;
@@ -978,7 +991,7 @@ int bdpt_render_direct(bdpt_ctx* c, const bdpt_frame_params* p, const bdpt_direc
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kCounterWords, st));
     HIP_TRY(hipEventRecord(c->ev0, st));
     if (fr.total_samples > 0)
-        HIP_TRY(launch_pt(c->sc, fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
+        HIP_TRY(launch_pt(pt_scene(c, p), fr, settings, fb, c->pt_levels, c->pt_ring, c->gstack, c->pt_nslots, c->work,
                           c->counters, c->pt_grid, st, c->pt_dparams));
     HIP_TRY(hipEventRecord(c->ev1, st));
     if ((rc = end_use(c, st))) return rc;

@@ -634,7 +634,9 @@ __device__ __forceinline__ void pt_resolve(PtLane& L, int res, float t, float u,
 }
 
 #if !BDPT_SAMPLER_STATE
-template <bool COUNT, bool OVERLAP>
+// SLACK: the overlapped walk's interior boxes with the ambiguity slack
+// (DevScene::node_slack, per render on the host; bdpt_frame_kernel's parameter)
+template <bool COUNT, bool OVERLAP, bool SLACK = true>
 __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const PtParams* __restrict__ pp) {
     const PtParams& P = *pp;
     __shared__ uint2 stack_mem[kLdsStack * 256];
@@ -711,7 +713,7 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
                 ts = trav_begin(tsc, L.ray);
                 tracing = true;
 #if PT_ROOT_LDS
-                if (root_in_lds && !walk_begin_lds<COUNT, true>(root_lds, L.ray, ri, false, ts, stk, cnt)) {
+                if (root_in_lds && !walk_begin_lds<COUNT, SLACK>(root_lds, L.ray, ri, false, ts, stk, cnt)) {
                     res = -1, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;  // no child hit: a miss
                     tracing = false;
                     has_res = true;
@@ -726,7 +728,7 @@ __global__ __launch_bounds__(256, PT_WAVES_PER_EU) void pt_frame_kernel(const Pt
             const bool at_leaf = (ts.link & kLeafBit) != 0;
             const uint64_t lv = __ballot(tracing && at_leaf);
             const bool do_leaf = popc64(lv) * 4 >= popc64(tr & ~lv) * PT_TRAV_SPLIT;
-            if (tracing && at_leaf == do_leaf && trav_step<COUNT>(tsc, L.ray, ri, false, ts, stk, cnt)) {
+            if (tracing && at_leaf == do_leaf && trav_step<COUNT, SLACK>(tsc, L.ray, ri, false, ts, stk, cnt)) {
                 res = ts.best, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;
                 tracing = false;
                 has_res = true;
@@ -825,10 +827,13 @@ hipError_t launch_pt(const dev::DevScene& sc, const dev::DevFrame& fr, const int
     if (e != hipSuccess) return e;
     const dev::PtParams* kp = static_cast<const dev::PtParams*>(dparams);
     const size_t lds = 4 * static_cast<size_t>(sc.lds_words);
-    const bool count = (fr.flags & 1u) != 0, overlap = host.ps.direct == 0;
-    if (count && overlap) hipLaunchKernelGGL((dev::pt_frame_kernel<true, true>), dim3(grid), dim3(256), lds, stream, kp);
+    const bool count = (fr.flags & 1u) != 0, overlap = host.ps.direct == 0, slack = sc.node_slack != 0;
+    // (the non-overlapped walk, traverse(), reads node_slack itself)
+    if (count && overlap && slack) hipLaunchKernelGGL((dev::pt_frame_kernel<true, true, true>), dim3(grid), dim3(256), lds, stream, kp);
+    else if (count && overlap) hipLaunchKernelGGL((dev::pt_frame_kernel<true, true, false>), dim3(grid), dim3(256), lds, stream, kp);
     else if (count) hipLaunchKernelGGL((dev::pt_frame_kernel<true, false>), dim3(grid), dim3(256), lds, stream, kp);
-    else if (overlap) hipLaunchKernelGGL((dev::pt_frame_kernel<false, true>), dim3(grid), dim3(256), lds, stream, kp);
+    else if (overlap && slack) hipLaunchKernelGGL((dev::pt_frame_kernel<false, true, true>), dim3(grid), dim3(256), lds, stream, kp);
+    else if (overlap) hipLaunchKernelGGL((dev::pt_frame_kernel<false, true, false>), dim3(grid), dim3(256), lds, stream, kp);
     else hipLaunchKernelGGL((dev::pt_frame_kernel<false, false>), dim3(grid), dim3(256), lds, stream, kp);
     return hipGetLastError();
 }
