@@ -274,6 +274,9 @@ struct KParams {
 // SLACK: interior boxes with slab_fast's ambiguity slack (DevScene::node_slack,
 // decided per render on the host); a template parameter so the node step of
 // the walk loop carries no branch on it.
+#ifndef BDPT_TAIL_PROBE
+#define BDPT_TAIL_PROBE 0  // measurement only (non-RR builds): the drain phase in the RR diag words (tools/tail_probe.py)
+#endif
 #ifndef BDPT_READY_HOIST
 #define BDPT_READY_HOIST 1  // the shade threshold read before the walk loop instead of in it (Caustic +0.85 %, synth1m +1.2 %)
 #endif
@@ -374,6 +377,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     bool coop_wait = false;  // a closest-hit walk begun, waiting for its turn to be walked by the whole wave
 #endif
     const uint64_t clock0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+#if BDPT_TAIL_PROBE && BDPT_RR != 1
+    uint64_t t_drain = 0, t_few = 0;  // wave-uniform (BDPT_TAIL_PROBE)
+#endif
 #ifndef BDPT_DIAG
 #define BDPT_DIAG 1  // 0: no timeline stamps (A/B only)
 #endif
@@ -473,6 +479,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             if (exhausted) break;
             continue;
         }
+#if BDPT_TAIL_PROBE && BDPT_RR != 1
+        if (exhausted) {  // the wave's drain: when it began, when at most 4 lanes were left busy
+            if (!t_drain) t_drain = __builtin_amdgcn_s_memrealtime();
+            if (!t_few && popc64(__ballot(BDPT_BUSY(L.state))) <= 4) t_few = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
 #if BDPT_OVERLAP
         // Overlapped schedule: lanes keep walking their query across loop
         // iterations; a lane whose query finished waits (result kept) until
@@ -680,6 +692,17 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         for (int k = 0; k < BDPT_EYE_SLOTS; k++) eye_slot_reset(kp.fb, k, -1);
 #endif
     if (BDPT_DIAG && lane0() && kpp->fr.diag) gmax(kpp->fr.diag + kDiagEnd, __builtin_amdgcn_s_memrealtime());
+#if BDPT_TAIL_PROBE && BDPT_RR != 1
+    // longest drain with <= 4 busy lanes, longest drain, their sum over waves, waves that had one
+    if (lane0() && kpp->fr.diag) {
+        const uint64_t end = __builtin_amdgcn_s_memrealtime();
+        unsigned long long* const d = kpp->fr.diag;
+        if (t_few) gmax(d + kDiagLongMax, static_cast<unsigned long long>(end - t_few));
+        if (t_drain) gmax(d + kDiagExpress1, static_cast<unsigned long long>(end - t_drain));
+        if (t_few) gadd(d + kDiagExpressCoop, static_cast<unsigned long long>(end - t_few));
+        if (t_few) gadd(d + kDiagExpressMore, 1ull);
+    }
+#endif
     if (COUNT) {
         if (lane0()) cnt.c[14] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - clock0);
         flush_counts(cnt, kp.counters);
