@@ -132,6 +132,34 @@ def test_gpu_translated_scene_matches_oracle(name, diags, tmp_path):
     assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
 
 
+@pytest.mark.parametrize("kind,diags", [("path", 250.0), ("path", 350.0), ("direct", 250.0), ("direct", 350.0)])
+def test_gpu_translated_scene_path_and_direct_match_oracle(kind, diags, tmp_path):
+    """The path tracer and the direct integrator take the same per-render choice
+    of interior-box test (bdpt_capi.cpp pt_scene): the Caustic scene moved ~250
+    and ~350 diagonals from 0 along (1, 1, 1), both sides of the condition."""
+    with open(variants.obj_path("caustic")) as f:
+        v = np.array([line.split()[1:4] for line in f if line.startswith("v ")], np.float64)
+    off = np.full(3, diags * np.linalg.norm(v.max(0) - v.min(0)))
+    path = variants.translated_obj("caustic", str(tmp_path), off)
+    cam = dict(variants.SCENES["caustic"]["camera"])
+    cam["eye"] = [float(np.float32(e + o)) for e, o in zip(cam["eye"], off)]
+    cam["at"] = [float(np.float32(a + o)) for a, o in zip(cam["at"], off)]
+    W, H, spp = 32, 24, 4
+    cfg = bdpt_amd.Config(camera=bdpt_amd.Camera(**cam), width=W, height=H, spp=spp)
+    sc = bdpt_amd.Scene(path)
+    if kind == "path":
+        fb = bdpt_amd.PathTracerIntegrator(sc, cfg, bdpt_amd.PathSettings()).render_frame().reshape(-1)
+        params = O.make_path_params(cam, W, H, spp)
+    else:
+        ds = bdpt_amd.DirectSettings(sampling_strategy="mis", emitter_samples=2, bsdf_samples=2)
+        fb = bdpt_amd.DirectIntegrator(sc, cfg, ds).render_frame().reshape(-1)
+        params = O.make_direct_params(cam, W, H, spp, strategy="mis", emitter_samples=2, bsdf_samples=2)
+    ref, _ = O.Scene(path).render(params)
+    assert (ref.reshape(-1, 3).sum(1) > 0).mean() > 0.2  # the box is in view
+    worst, exact, _ = report(fb, ref.reshape(-1))
+    assert worst <= TOL, f"max per-pixel rel L2 {worst:.3g} (bit-exact {exact:.4f})"
+
+
 @pytest.mark.parametrize("name,W,H,spp,rr", [
     ("caustic", 24, 40, 3, 1),    # rrDepth 1: both walks stop at once (2 draws)
     ("caustic", 24, 40, 3, 2),
