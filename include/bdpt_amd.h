@@ -417,8 +417,9 @@ typedef struct {
  * result in hit only. The traversal is the frame kernels' (culled 4-wide tree,
  * reference-leaf check; origins beyond 100 scene diagonals walk the reference's
  * tree unculled), with the interior-box test a frame would use for the batch's
- * origins: without the ambiguity slack when all lie within 100 scene diagonals,
- * with it otherwise. */
+ * origins: without the ambiguity slack when all lie within 100 scene diagonals
+ * and, like the scene box, within 300 diagonals of 0 (the slack-free test's
+ * fma planes), with it otherwise. */
 int bdpt_intersect(bdpt_ctx* ctx, int64_t n, const float* rays, int32_t occlusion, bdpt_hit* out);
 /* The same with the frame kernels' near-cull rule: origin_normals (n x 3) is the
  * normal of the surface each ray leaves (a path vertex's interpolated shading
