@@ -56,7 +56,7 @@ constexpr int kBlock = 256;
 #define BDPT_OVERLAP 1  // overlapped walk / shade schedule in the megakernel (0: one query then shade, in lockstep)
 #endif
 #ifndef BDPT_TRAV_SPLIT
-#define BDPT_TRAV_SPLIT 6  // > 0: leaf and interior-node steps in separate iterations (leaf step if 4 * leaf lanes >= SPLIT * node lanes; round 5 re-sweep: 6 over 8)
+#define BDPT_TRAV_SPLIT 8  // > 0: leaf and interior-node steps in separate iterations (leaf step if 4 * leaf lanes >= SPLIT * node lanes; round 5: 6 over 8, then 8 over 6 / 10 / 12 once node steps also follow leaf iterations)
 #endif
 #ifndef BDPT_SEED_CHUNK
 #define BDPT_SEED_CHUNK 1  // refill from per-wave chunks of 64 samples seeded together (0: per-refill seeding)
@@ -274,6 +274,9 @@ struct KParams {
 // SLACK: interior boxes with slab_fast's ambiguity slack (DevScene::node_slack,
 // decided per render on the host); a template parameter so the node step of
 // the walk loop carries no branch on it.
+#ifndef BDPT_UNROLL_ANY
+#define BDPT_UNROLL_ANY 1  // the extra node step also after a leaf iteration, for lanes that popped to an interior node (with split 8: Caustic +1.0 %, HardLight +1.8 %, synth1m +1.0 %)
+#endif
 #ifndef BDPT_TAIL_PROBE
 #define BDPT_TAIL_PROBE 0  // measurement only (non-RR builds): the drain phase in the RR diag words (tools/tail_probe.py)
 #endif
@@ -646,7 +649,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             // BDPT_WALK_UNROLL more interior-node steps before the wave's ballots
 #pragma unroll
             for (int k = 0; k < BDPT_WALK_UNROLL; k++)
-                if (!do_leaf && tracing && !fin && !(ts.link & kLeafBit))
+                if ((BDPT_UNROLL_ANY || !do_leaf) && tracing && !fin && !(ts.link & kLeafBit))
                     fin = trav_step<COUNT, SLACK>(tsc, L.ray, ri, q_any, ts, stk, cnt);
             if (fin) {
 #else
