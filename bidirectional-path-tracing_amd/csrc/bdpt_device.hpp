@@ -1536,6 +1536,74 @@ __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, 
     return ok;
 }
 
+// coop_closest for up to four rays at once: the wave split into 64 / G groups
+// of G lanes (G = 32 or 16), group g walking its own ray on its own range
+// [base, base + cap) of the stack entries; inactive groups idle. Each group's
+// result is coop_closest's for its ray (the same per-entry tests, the minimum
+// (t, index) over the group's candidates); false for a group whose entries did
+// not fit. For the Russian-roulette build's express waves holding 2-4 long walks,
+// which otherwise take turns with all 64 lanes.
+template <bool SLACK>
+__device__ __forceinline__ bool coop_closest_groups(const TravScene& sc, const Ray& r, const RayInv& ri, float bound,
+                                                    bool active, CoopStack stk, int base, int cap, int G,
+                                                    float& best_t, int& best, float& best_u, float& best_v) {
+    const uint32_t lane = __lane_id();
+    const int gl = static_cast<int>(lane) & (G - 1);
+    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (static_cast<int>(lane) - gl);
+    best_t = bound < r.max_t ? bound : r.max_t, best = -1, best_u = best_v = 0.f;
+    if (active && gl == 0) *stk.at(base) = u32x2{sc.wroot_link, __float_as_uint(-__builtin_inff())};
+    int sp = active ? 1 : 0;
+    bool ok = true;
+    while (__ballot(sp > 0)) {
+        const int k = sp < G ? sp : G;
+        u32x2 e = {kEmptyLinkDev, 0u};
+        if (gl < k) e = *stk.at(base + sp - k + gl);
+        sp -= k;
+        const float far = cull_far(best_t);
+        const bool live = e.x != kEmptyLinkDev && !(__uint_as_float(e.y) > far);
+        float lt = best_t, lu = best_u, lv = best_v;
+        int lb = best;
+        float key[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+        uint32_t lnk[4] = {kEmptyLinkDev, kEmptyLinkDev, kEmptyLinkDev, kEmptyLinkDev};
+        if (live) {
+            if (e.x & kLeafBit) {
+                Counts cnt;  // (not a counting pass)
+                wleaf_tests<false>(sc.wtri, sc.lbox, e.x, r, ri, false, lt, lb, lu, lv, cnt);
+            } else {
+                node_child_keys<SLACK>(load_wnode(sc.wnodes, e.x), r, ri, far, key, lnk);
+            }
+        }
+        // each group's lexicographic minimum of (t, index) over its improving lanes
+        uint64_t imp = __ballot(lb != best);
+        if (imp) {
+            uint64_t m = ~0ull;
+            int w = static_cast<int>(lane);
+            while (imp) {
+                const int i = __ffsll(static_cast<unsigned long long>(imp)) - 1;
+                imp &= imp - 1;
+                const uint64_t ki = coop_key(__shfl(lt, i), __shfl(lb, i));
+                if ((gmask >> i) & 1ull && ki < m) m = ki, w = i;
+            }
+            best_t = __shfl(lt, w), best = __shfl(lb, w), best_u = __shfl(lu, w), best_v = __shfl(lv, w);
+        }
+        // children far-first, each group on its own range
+#pragma unroll
+        for (int c = 3; c >= 0; c--) {
+            const uint64_t has = __ballot(lnk[c] != kEmptyLinkDev) & gmask;
+            const int pos = sp + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                     static_cast<uint32_t>(has >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(has), 0u)));
+            const int n = popc64(has);
+            if (sp + n > cap) {
+                ok = false;
+            } else if (lnk[c] != kEmptyLinkDev) {
+                *stk.at(base + pos) = u32x2{lnk[c], __float_as_uint(key[c])};
+            }
+            if (sp + n <= cap) sp += n;
+        }
+    }
+    return ok;
+}
+
 // AcceleratorBVH::intersect's shading of a closest hit (accel.h:133-166).
 __device__ __forceinline__ void shade_hit(const DevScene& sc, int i, float u, float v, float t, f3 dir, Hit& h) {
     const float4* sh = sc.shade + kShadeStride * static_cast<size_t>(i);

@@ -277,6 +277,9 @@ struct KParams {
 #ifndef BDPT_UNROLL_ANY
 #define BDPT_UNROLL_ANY 1  // the extra node step also after a leaf iteration, for lanes that popped to an interior node (with split 8: Caustic +1.0 %, HardLight +1.8 %, synth1m +1.0 %)
 #endif
+#ifndef BDPT_COOP_GROUPS
+#define BDPT_COOP_GROUPS 1  // express waves with 2-4 long walks walk them at once in groups of 32 / 16 lanes (coop_closest_groups; RR Caustic frames 42.7-45.2 s vs 43.8-54.0)
+#endif
 #ifndef BDPT_TAIL_PROBE
 #define BDPT_TAIL_PROBE 0  // measurement only (non-RR builds): the drain phase in the RR diag words (tools/tail_probe.py)
 #endif
@@ -570,6 +573,61 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // in their turn: a walk begun while another lane still walks alone waits too.
         if (!COUNT && express) {
             const uint64_t busy = __ballot(BDPT_BUSY(L.state)), wt = __ballot(coop_wait), bg = __ballot(began);
+#if BDPT_COOP_GROUPS
+            if (popc64(busy) >= 2 && popc64(busy) <= BDPT_COOP_MAX && (bg | wt) == busy) {
+                // 2-4 long walks: each walked by its own group of 32 or 16 lanes, all at once
+                const int kb = popc64(busy), G = kb == 2 ? 32 : 16;
+                const int me = static_cast<int>(opaque_tid() & 63), gi = me / G;
+                int src = -1;  // the lane whose walk this lane's group takes: the gi-th busy lane
+                {
+                    uint64_t m = busy;
+                    for (int g = 0; g < 4 && m; g++) {
+                        const int bit = __ffsll(static_cast<unsigned long long>(m)) - 1;
+                        if (gi == g) src = bit;
+                        m &= m - 1;
+                    }
+                }
+                const bool act = src >= 0;
+                const int sl = act ? src : me;
+                Ray q;
+                q.o = mk(__shfl(L.ray.o.x, sl), __shfl(L.ray.o.y, sl), __shfl(L.ray.o.z, sl));
+                q.d = mk(__shfl(L.ray.d.x, sl), __shfl(L.ray.d.y, sl), __shfl(L.ray.d.z, sl));
+                q.min_t = __shfl(L.ray.min_t, sl), q.max_t = __shfl(L.ray.max_t, sl);
+                RayInv qi;
+                qi.inv = mk(__shfl(ri.inv.x, sl), __shfl(ri.inv.y, sl), __shfl(ri.inv.z, sl));
+                qi.near = __shfl(ri.near, sl);
+                qi.fast = true;
+                const float guess = BDPT_GRAZE_IN_DIST ? -1.f : __shfl(L.h.dist, sl);
+                const CoopStack cs{stack_mem + (threadIdx.x & ~63u), kBlock};
+                const int cap = kLdsStack * G, gbase = gi * cap;
+                const bool bounded = act && guess > 0.f;
+                float t = 0.f, u = 0.f, v = 0.f;
+                int r = -1;
+                bool ok = coop_closest_groups<SLACK>(tsc, q, qi, bounded ? 2.f * guess : q.max_t, act, cs, gbase, cap, G,
+                                                     t, r, u, v);
+                const bool again = bounded && ok && r < 0;  // nothing below the bound: the walk unbounded
+                if (__ballot(again)) {
+                    float t2 = 0.f, u2 = 0.f, v2 = 0.f;
+                    int r2 = -1;
+                    const bool ok2 = coop_closest_groups<SLACK>(tsc, q, qi, q.max_t, again, cs, gbase, cap, G, t2, r2, u2, v2);
+                    if (again) t = t2, u = u2, v = v2, r = r2, ok = ok2;
+                }
+                // each walk's owner takes its group's result (group = the owner's rank among the busy lanes)
+                const int rl = (BDPT_BUSY(L.state) ? lanes_below(busy) : 0) * G;
+                t = __shfl(t, rl), u = __shfl(u, rl), v = __shfl(v, rl), r = __shfl(r, rl);
+                ok = __shfl(ok ? 1 : 0, rl) != 0;
+                if (BDPT_BUSY(L.state)) {
+                    coop_wait = false;
+                    if (ok) {
+                        res = r, rt = t, ru = u, rv = v;
+                        tracing = false;
+                        has_res = true;
+                    } else {
+                        ts = trav_begin(tsc, L.ray);  // its stack columns were the wave's
+                    }
+                }
+            } else
+#endif
             if (popc64(busy) <= BDPT_COOP_MAX && (bg | wt) == busy) {
                 const int b = __ffsll(static_cast<unsigned long long>(wt ? wt : bg)) - 1;
                 const int me = static_cast<int>(opaque_tid() & 63);
