@@ -116,7 +116,7 @@ constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227
 // HardLight rrDepth 2 / 3 / 4 / 5: +12.5 / +4.4 / +1.2 / -0.2 %).
 // BDPT_SPLIT_MAX_RR overrides the threshold (0: never).
 constexpr int kSplitMaxRrDepth = 3;
-constexpr int64_t kDeepSceneTris = 262144;  // scenes from this many triangles shade at 40 ready lanes
+constexpr int64_t kDeepSceneTris = 262144;  // scenes from this many triangles shade at 36 ready lanes (their walks are longer)
 static bool use_split_build(int rr_depth) {
     const char* e = std::getenv("BDPT_SPLIT_MAX_RR");  // read per render (tests force either build)
     return rr_depth <= (e ? std::atoi(e) : kSplitMaxRrDepth);
@@ -770,7 +770,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     // triangles: longer walks) shades at 40 ready lanes, others at 44 (round 5:
     // synth1m 1024^2x64 191.8 vs 188.5 Msamples/s at 40 / 44; Caustic and HardLight
     // 0.3-0.8 % slower at 40). BDPT_SHADE_READY overrides it (sweeps).
-    fr.shade_ready = c->ntri >= kDeepSceneTris ? 40 : 44;
+    fr.shade_ready = c->ntri >= kDeepSceneTris ? 36 : 44;
     if (const char* e = std::getenv("BDPT_SHADE_READY")) fr.shade_ready = std::max(1, std::min(64, std::atoi(e)));
     dev::DevScene sc = c->sc;
     sc.node_slack = node_slack_needed(c, eye, 1);
