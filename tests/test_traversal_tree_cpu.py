@@ -139,3 +139,19 @@ def test_greedy_collapse_tree_preconditions_and_dp_is_smaller(scene_name, monkey
     a, b = dp.info(), greedy.info()
     assert a["wide_leaves"] == b["wide_leaves"]
     assert a["wide_nodes"] <= b["wide_nodes"]
+
+
+@pytest.mark.parametrize("name,diags", [("caustic", 250.0), ("caustic", 350.0), ("hardlight", 100.0)])
+def test_tree_preconditions_on_translated_scenes(name, diags, tmp_path):
+    """The scenes test_gpu_parity.py's translated-scene cases render: every vertex
+    moved ~diags scene diagonals from 0 (variants.translated_obj), so float
+    coordinates are coarse relative to the scene, and the padded boxes must still
+    hold their triangles (the slack-free interior test's precondition there)."""
+    with open(variants.obj_path(name)) as f:
+        v = np.array([line.split()[1:4] for line in f if line.startswith("v ")], np.float64)
+    off = np.full(3, diags * np.linalg.norm(v.max(0) - v.min(0)))
+    path = variants.translated_obj(name, str(tmp_path), off)
+    with open(path) as f:
+        w = np.array([line.split()[1:4] for line in f if line.startswith("v ")], np.float64)
+    assert w.shape == v.shape and np.abs(w - v - off).max() < 1e-5
+    check_tree(bdpt_amd.Scene(path), tri_tree=True)
