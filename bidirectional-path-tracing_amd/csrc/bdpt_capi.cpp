@@ -680,6 +680,7 @@ static int check_params(const bdpt_frame_params* p) {
     return BDPT_OK;
 }
 
+constexpr int kExpressDepth = 512;  // Russian roulette: express mode past this many bounces
 static dev::DevFrame make_frame(const bdpt_frame_params* p) {
     dev::DevFrame fr{};
     camera_constants(p->camera.eye, p->camera.at, p->camera.up, p->camera.fov, p->width, p->height, fr.cam);
@@ -697,6 +698,12 @@ static dev::DevFrame make_frame(const bdpt_frame_params* p) {
     fr.inv_pixels = 1.f / static_cast<float>(fr.W * fr.H);
     fr.capped = nullptr;  // the context's word, set by the caller
     fr.diag = nullptr;    // the context's timeline, set by bdpt_render
+    // Russian-roulette schedule (bdpt_kernels.hip express mode): BDPT_EXPRESS_DEPTH and
+    // BDPT_COOP_GROUPS=0 override the build's depth and grouped walks (tests reach the
+    // grouped and turn-taking walks on small frames this way; the results are the same)
+    fr.express_depth = kExpressDepth;
+    if (const char* e = std::getenv("BDPT_EXPRESS_DEPTH")) fr.express_depth = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("BDPT_COOP_GROUPS")) fr.sched_flags |= *e == '0' ? dev::kSchedNoCoopGroups : 0u;
     return fr;
 }
 
@@ -735,7 +742,8 @@ static uint32_t node_slack_needed(const bdpt_ctx* c, const float* const* origins
     if (!(diag2 > 0.0) || !std::isfinite(diag2)) return 1u;
     // BDPT_SLAB_SIGN builds address the node planes by 32-bit offsets (load_wnode_nf)
     if (BDPT_SLAB_SIGN && c->wnode_bytes >= (int64_t{1} << 32)) return 1u;
-    const double coord_max = BDPT_SLAB_FMA || BDPT_SLAB_SIGN ? kFmaCoordDiags * std::sqrt(diag2) : HUGE_VAL;
+    constexpr bool kFmaPlanes = BDPT_SLAB_FMA != 0 || BDPT_SLAB_SIGN != 0;
+    const double coord_max = kFmaPlanes ? kFmaCoordDiags * std::sqrt(diag2) : HUGE_VAL;
     for (int a = 0; a < 3; a++)
         if (!(std::fabs(c->box_lo[a]) <= coord_max && std::fabs(c->box_hi[a]) <= coord_max)) return 1u;
     for (int k = 0; k < n; k++) {
@@ -766,10 +774,11 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
         return fail(BDPT_ERR_UNSUPPORTED, "rr_depth > 28 or Russian roulette with BSDF records in HBM (too many "
                                           "materials for the LDS table) is not built");
     if ((rc = ensure_lv(c, fr.lv_max, c->nslots))) return rc;
-    // Shading threshold of the frame kernels: a scene whose tree is deep (many
-    // triangles: longer walks) shades at 40 ready lanes, others at 44 (round 5:
-    // synth1m 1024^2x64 191.8 vs 188.5 Msamples/s at 40 / 44; Caustic and HardLight
-    // 0.3-0.8 % slower at 40). BDPT_SHADE_READY overrides it (sweeps).
+    // Shading threshold of the frame kernels: a scene whose tree is deep (from
+    // kDeepSceneTris triangles: longer walks) shades at 36 ready lanes, others at 44
+    // (round 5, r5m / r5ag: synth1m 1024^2x64 191.8 vs 188.5 Msamples/s at 40 / 44,
+    // then 205.6 / 205.1 / 205.2 at 36 vs 203.8 / 203.3 / 204.6 at 40; Caustic and
+    // HardLight 0.3-0.8 % slower below 44). BDPT_SHADE_READY overrides it (sweeps).
     fr.shade_ready = c->ntri >= kDeepSceneTris ? 36 : 44;
     if (const char* e = std::getenv("BDPT_SHADE_READY")) fr.shade_ready = std::max(1, std::min(64, std::atoi(e)));
     dev::DevScene sc = c->sc;

@@ -179,8 +179,15 @@ struct DevFrame {
     // lanes with a finished query that trigger a wave's shading step (the frame
     // kernels; chosen per render by the host: 0 = the build's BDPT_SHADE_READY)
     int32_t shade_ready;
+    // Russian-roulette build: a subpath deeper than express_depth bounces puts its
+    // wave in express mode (bdpt_kernels.hip); sched_flags kSchedNoCoopGroups walks
+    // express waves' 2-4 long walks in turn instead of in lane groups. Schedule
+    // only: the same per-sample arithmetic either way (tests/test_gpu_express.py).
+    int32_t express_depth;
+    uint32_t sched_flags;
 };
 enum : uint32_t { kParkOn = 1u, kParkResume = 2u };
+enum : uint32_t { kSchedNoCoopGroups = 1u };
 
 struct Ray {
     f3 o, d;
@@ -511,8 +518,10 @@ __device__ __forceinline__ f3 phong_lobe(F2 u, float ex) {
     const SinCos sc = glibc_sincosf2(phi);
     return mk(sinTheta * sc.c, sinTheta * sc.s, cosTheta);
 }
+// EXACT: glibc's powf even in the fast-weight builds (the BSDF sampler, below)
+template <bool EXACT = false>
 __device__ __forceinline__ float phong_lobe_pdf(f3 v, float ex) {
-    return v.z >= 0.f ? (ex + 2) * kInvTwoPi * pow_w(v.z, ex) : 0.f;
+    return v.z >= 0.f ? (ex + 2) * kInvTwoPi * (EXACT ? glibc_powf(v.z, ex) : pow_w(v.z, ex)) : 0.f;
 }
 // squareToUniformTriangle (math.h:229-234)
 __device__ __forceinline__ F2 uniform_triangle(F2 s) {
@@ -1647,6 +1656,7 @@ __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]);
 // MixtureBSDF::eval == PhongBSDF::eval (mixture.h:59-75, phong.h:56-71).
 // With Ks == 0 the specular term is (0 * (n + 2)) * INV_TWOPI * powf(c, n) = +0
 // (powf of c in [0, 1] is finite), and val + 0 == val: skipping it is exact.
+template <bool EXACT = false>
 __device__ __forceinline__ f3 glossy_eval(const BsdfRecord& b, f3 wi, f3 wo) {
     f3 val = mk(0.f, 0.f, 0.f);
     if (wi.z >= 0.f && wo.z >= 0.f) {
@@ -1654,7 +1664,7 @@ __device__ __forceinline__ f3 glossy_eval(const BsdfRecord& b, f3 wi, f3 wo) {
         if (b.ks[0] != 0.f || b.ks[1] != 0.f || b.ks[2] != 0.f) {
             const float ex = b.exponent;
             const float c = glibc_fminf(glibc_fmaxf(dot(wi, reflect_z(wo)), 0.f), 1.f);
-            val = val + ((ld3(b.ks) * (ex + 2)) * kInvTwoPi) * pow_w(c, ex);
+            val = val + ((ld3(b.ks) * (ex + 2)) * kInvTwoPi) * (EXACT ? glibc_powf(c, ex) : pow_w(c, ex));
         }
         val = val * b.scale;
         val = val * wi.z;
@@ -1676,11 +1686,12 @@ __device__ __forceinline__ f3 bsdf_eval(const BsdfRecord& b, f3 wi, f3 wo) {
     return mk(0.f, 0.f, 0.f);  // delta lobes (perfectmirror.h:41-47, glass.h:55-59)
 }
 
+template <bool EXACT = false>
 __device__ __forceinline__ float phong_part_pdf(const BsdfRecord& b, f3 wi, f3 wo) {
     f3 rs, rt;
     const f3 rn = reflect_z(wo);
     make_frame(rn, rs, rt);
-    return phong_lobe_pdf(to_local(rs, rt, rn, wi), b.exponent);
+    return phong_lobe_pdf<EXACT>(to_local(rs, rt, rn, wi), b.exponent);
 }
 
 // With specw == 0, pdfPhong * 0 = +0 (pdfPhong is finite and >= 0) and
@@ -1805,6 +1816,10 @@ __device__ BDPT_NOINLINE f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f
             return mk(1.f, 1.f, 1.f);
         case BSDF_GLASS:
             return glass_sample(b, wo, u, wi, pdf);
+        // The sampled value steers the walk (ContinuePathRandomWalk ends it on f == 0,
+        // bdpt.h:253), so the Phong powers here stay glibc's powf in every build: the
+        // fast-weight pow_w flushes results below 2^-126 to 0, which for a
+        // lobe with Kd = 0 would end a path the reference continues.
         case BSDF_MIXTURE: {  // mixture.h:102-151
             f3 val;
             if (u.x < b.specw) {
@@ -1813,13 +1828,13 @@ __device__ BDPT_NOINLINE f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f
                 const f3 rn = reflect_z(wo);
                 make_frame(rn, rs, rt);
                 wi = to_world(rs, rt, rn, phong_lobe(ns, b.exponent));
-                val = bsdf_eval(b, wi, wo);
             } else {
                 const F2 ns{div_cr(u.x - b.specw, 1.f - b.specw), u.y};
                 wi = cosine_hemisphere(ns);
-                val = bsdf_eval(b, wi, wo);
             }
-            pdf = bsdf_pdf(b, wi, wo);
+            val = glossy_eval<true>(b, wi, wo);
+            if (b.specw == 0.f) pdf = cosine_hemisphere_pdf(wi);  // bsdf_pdf's exact shortcut
+            else pdf = (phong_part_pdf<true>(b, wi, wo) * b.specw) + (cosine_hemisphere_pdf(wi) * (1.f - b.specw));
             return val;
         }
         case BSDF_PHONG: {  // phong.h:85-100
@@ -1827,9 +1842,9 @@ __device__ BDPT_NOINLINE f3 bsdf_sample_call(const BsdfRecord& b, f3 wo, F2 u, f
             const f3 rn = reflect_z(wo);
             make_frame(rn, rs, rt);
             const f3 ls = phong_lobe(u, b.exponent);
-            pdf = phong_lobe_pdf(ls, b.exponent);
+            pdf = phong_lobe_pdf<true>(ls, b.exponent);
             wi = to_world(rs, rt, rn, ls);
-            return bsdf_eval(b, wi, wo);
+            return glossy_eval<true>(b, wi, wo);
         }
         default:  // null BSDF (illum 5): the reference dereferences nullptr
             pdf = 0.f;

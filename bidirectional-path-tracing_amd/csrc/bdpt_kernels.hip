@@ -74,7 +74,7 @@ constexpr int kBlock = 256;
 #define BDPT_TAIL_FRAC 6  // (measured, 512x512x256 1/8 shard: end tail 2.19 -> 1.93 ms, steady state unchanged)
 #endif
 #ifndef BDPT_EXPRESS_DEPTH
-#define BDPT_EXPRESS_DEPTH 512  // Russian-roulette build: a subpath this deep puts its wave in express mode (below)
+#define BDPT_EXPRESS_DEPTH 512  // Russian-roulette build: a subpath this deep puts its wave in express mode (below; DevFrame::express_depth, set per render)
 #endif
 #ifndef BDPT_ROOT_LDS
 #define BDPT_ROOT_LDS 1  // 1: the traversal root and its interior children in LDS, tested when a walk begins (RootLds; measured +1.6 %)
@@ -574,7 +574,8 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         if (!COUNT && express) {
             const uint64_t busy = __ballot(BDPT_BUSY(L.state)), wt = __ballot(coop_wait), bg = __ballot(began);
 #if BDPT_COOP_GROUPS
-            if (popc64(busy) >= 2 && popc64(busy) <= BDPT_COOP_MAX && (bg | wt) == busy) {
+            if (!(P->fr.sched_flags & kSchedNoCoopGroups) && popc64(busy) >= 2 && popc64(busy) <= BDPT_COOP_MAX &&
+                (bg | wt) == busy) {
                 // 2-4 long walks: each walked by its own group of 32 or 16 lanes, all at once
                 const int kb = popc64(busy), G = kb == 2 ? 32 : 16;
                 const int me = static_cast<int>(opaque_tid() & 63), gi = me / G;
@@ -731,7 +732,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const uint32_t act = resolve<COUNT>(L, res, rt, ru, rv, P->sc, P->fr, P->fb, cnt);
             if (COUNT && first_active_lane()) cnt.c[20] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - r0);
             advance<COUNT>(L, act, P->sc, P->fr, P->fb, ls, cnt);
-            if (BDPT_RR == 1) long_walk = L.state != ST_IDLE && L.c.depth > BDPT_EXPRESS_DEPTH;
+            if (BDPT_RR == 1) long_walk = L.state != ST_IDLE && L.c.depth > P->fr.express_depth;
         }
         if (COUNT && first_active_lane()) {
             const uint64_t c2 = __builtin_amdgcn_s_memtime();

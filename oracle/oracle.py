@@ -221,8 +221,8 @@ def walk_stats(reset: bool = True) -> dict:
 
 
 def counters(reset: bool = True) -> dict:
-    out = (ctypes.c_int64 * 8)()
+    out = (ctypes.c_int64 * 9)()
     lib().tro_counters(out, 1 if reset else 0)
     keys = ["closest_rays", "shadow_rays", "interior_visits", "tri_tests", "light_verts",
-            "light_vert_reads", "splats", "rng_draws"]
+            "light_vert_reads", "splats", "rng_draws", "eye_retraces"]
     return dict(zip(keys, list(out)))

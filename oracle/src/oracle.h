@@ -80,7 +80,8 @@ void tro_sample(const tro_scene* s, const tro_params* p, int pixel, int k, float
  * byte model of SURVEY.md §8(d)): [0] closest-hit rays, [1] shadow rays,
  * [2] interior-node visits, [3] triangle tests, [4] light vertices stored,
  * [5] light-vertex reads in connections, [6] splats, [7] RNG draws. */
-void tro_counters(int64_t out[8], int reset);
+#define TRO_NUM_COUNTERS 9
+void tro_counters(int64_t out[TRO_NUM_COUNTERS], int reset);
 
 /* Light vertices dropped because a subpath outgrew the oracle's 1024-vertex
  * store (Russian roulette only; always 0 in practice). */

@@ -24,9 +24,13 @@
 #include "tr_internal.h"
 
 /* ---------------------------------------------------------------- counters */
-static __thread int64_t g_ctr[8];
-void tro_counters(int64_t out[8], int reset) {
-    for (int i = 0; i < 8; i++) out[i] = g_ctr[i];
+/* [0] closest rays, [1] shadow rays, [2] interior visits, [3] triangle tests,
+ * [4] light vertices stored, [5] light-vertex reads (connectVertices calls),
+ * [6] splats, [7] RNG draws, [8] eye walks whose first intersect re-traces the
+ * primary ray (bdpt.h:70 repeats :225; the GPU reuses that hit instead). */
+static __thread int64_t g_ctr[TRO_NUM_COUNTERS];
+void tro_counters(int64_t out[TRO_NUM_COUNTERS], int reset) {
+    for (int i = 0; i < TRO_NUM_COUNTERS; i++) out[i] = g_ctr[i];
     if (reset) memset(g_ctr, 0, sizeof g_ctr);
 }
 
@@ -769,6 +773,7 @@ static v3 eye_walk(const ctx_t* c, const pvert_t* lverts, int nl, ray_t ray, tr_
     float rrp = 1.f;
     while (walk_continues(c, depth, rrp, smp)) {
         hit_t hit;
+        if (depth == 1 && 1 < c->rr_depth) g_ctr[8]++;
         if (!scene_intersect(s, &wi, &hit)) break;
         float distSquared = hit.t * hit.t;
         float absCosIn = fabsf(hit.wo.z);
