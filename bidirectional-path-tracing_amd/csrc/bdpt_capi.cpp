@@ -108,6 +108,7 @@ const char* debug_knob(const char* name) {
     } while (0)
 
 constexpr int kCounterWords = BDPT_NUM_COUNTERS + 3 + 4;  // sums, the counting pass's 3 maxima (Counts::m), the task histogram (Counts::q)
+constexpr uint32_t kTaskCap = 256;  // shadow-ray tasks per wave ring (a power of two; DevFrame::tasks)
 constexpr int kLazyRrDepth = 28;  // lazy MT19937 covers 10 + 8 * 27 = 226 < 227 draws
 // Short subpaths run the BDPT_SPLIT_CONTINUE build (bdpt_kernels_split.hip): the
 // ST_DEFER step it removes is one loop slot of the ~(rrDepth + 1)^2 / 2 a sample
@@ -215,6 +216,7 @@ struct bdpt_ctx {
     uint32_t* pt_ring = nullptr;
     uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28, RR)
     uint32_t* park = nullptr;     // Russian roulette: continuation records + parked-slot list (DevFrame::park)
+    float4* tasks = nullptr;      // per-wave shadow-ray task rings (DevFrame::tasks; read by BDPT_HELP builds)
     unsigned long long work_init = 0;  // BDPT_SAMPLE_RANGE's first sample (host copy for the async upload)
     uint32_t* capped = nullptr;   // samples that met the Russian-roulette bounds, per call
     unsigned long long* diag = nullptr;  // the BDPT frame kernel's timeline (dev::kDiag*)
@@ -505,7 +507,7 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
                     static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
                     static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state), static_cast<void*>(c->capped),
                     static_cast<void*>(c->diag),
-                    static_cast<void*>(c->splat_list), static_cast<void*>(c->park)})
+                    static_cast<void*>(c->splat_list), static_cast<void*>(c->park), static_cast<void*>(c->tasks)})
         if (p) (void)hipFree(p);
     if (c->last_use) (void)hipEventDestroy(c->last_use);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -660,6 +662,9 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     c->sc.gdepth = static_cast<uint32_t>(std::max(1, depth - lds_entries));  // per slot (DevScene::gdepth)
     const size_t spill_mega = static_cast<size_t>(c->sc.gdepth) * c->nslots;
     HIP_TRY(hipMalloc(&c->gstack, sizeof(uint2) * std::max<size_t>(1, spill_mega)));
+    // shadow-ray task rings, one per wave of the persistent grid (4096 waves x 256 x 48 B = 50 MB on
+    // 256 CUs); only builds with BDPT_HELP read them
+    HIP_TRY(hipMalloc(&c->tasks, sizeof(float4) * 3 * kTaskCap * (c->nslots / 64)));
     *out = c.release();
     return BDPT_OK;
 }
@@ -702,6 +707,7 @@ static dev::DevFrame make_frame(const bdpt_frame_params* p) {
     // BDPT_COOP_GROUPS=0 override the build's depth and grouped walks (tests reach the
     // grouped and turn-taking walks on small frames this way; the results are the same)
     fr.express_depth = kExpressDepth;
+    fr.task_cap = kTaskCap;
     if (const char* e = std::getenv("BDPT_EXPRESS_DEPTH")) fr.express_depth = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("BDPT_COOP_GROUPS")) fr.sched_flags |= *e == '0' ? dev::kSchedNoCoopGroups : 0u;
     return fr;
@@ -767,6 +773,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     dev::DevFrame fr = make_frame(p);
     fr.capped = c->capped;
+    fr.tasks = c->tasks;
     const bool hbm = c->sc.lds_bsdf_off == dev::kNoLds;
     const bool rr = fr.rr_mode != 0;
     const float* eye[1] = {p->camera.eye};

@@ -185,6 +185,10 @@ struct DevFrame {
     // only: the same per-sample arithmetic either way (tests/test_gpu_express.py).
     int32_t express_depth;
     uint32_t sched_flags;
+    // Shadow-ray task rings of the BDPT_HELP build (bdpt_path.hpp task_push): per
+    // wave task_cap records of 48 bytes (3 float4), wave w's at tasks + 3 * task_cap * w
+    float4* tasks;
+    uint32_t task_cap;
 };
 enum : uint32_t { kParkOn = 1u, kParkResume = 2u };
 enum : uint32_t { kSchedNoCoopGroups = 1u };
@@ -879,6 +883,12 @@ enum : int { kDiagStart = 0, kDiagLastClaim = 1, kDiagEnd = 2, kDiagErrors = 3, 
 // here: mixed with int in min / max it selected the double overloads, and the
 // refill and shade-threshold arithmetic ran in f64.)
 __device__ __forceinline__ int popc64(uint64_t m) { return __builtin_popcountll(m); }
+// The lane's rank among the set lanes of m below it (mbcnt: no per-lane mask
+// held across the loop).
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
+}
 
 // SIMD-efficiency probe: true on the lowest active lane of the wave only.
 __device__ __forceinline__ bool first_active_lane() {

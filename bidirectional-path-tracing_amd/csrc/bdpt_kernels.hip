@@ -39,6 +39,14 @@
 #endif
 #endif
 
+// Shadow-ray tasks walked by waiting lanes (bdpt_path.hpp task_push): only the
+// overlapped frame kernels without Russian roulette build them.
+#if (defined(BDPT_RR) && BDPT_RR) || (defined(BDPT_SAMPLER_STATE) && BDPT_SAMPLER_STATE) || \
+    (defined(BDPT_OVERLAP) && !BDPT_OVERLAP)
+#undef BDPT_HELP
+#define BDPT_HELP 0
+#endif
+
 // The eye-estimate slots (bdpt_path.hpp) are claimed with the 64-sample chunks.
 #if defined(BDPT_SEED_CHUNK) && !BDPT_SEED_CHUNK && !defined(BDPT_EYE_SLOTS)
 #define BDPT_EYE_SLOTS 0
@@ -289,12 +297,7 @@ struct KParams {
 #ifndef BDPT_TID_REMAT
 #define BDPT_TID_REMAT 1  // the lane's traversal-stack and light-vertex addresses re-derived from threadIdx.x at each use
 #endif
-// The lane's rank among the set lanes of m below it (mbcnt: no per-lane mask
-// held across the loop), and "this is lane 0" from an opaque threadIdx.x.
-__device__ __forceinline__ int lanes_below(uint64_t m) {
-    return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
-}
+// "this is lane 0" from an opaque threadIdx.x (lanes_below: bdpt_device.hpp).
 __device__ __forceinline__ bool lane0() { return (opaque_tid() & 63) == 0; }
 #ifndef BDPT_TAIL_CHUNK
 #define BDPT_TAIL_CHUNK 4  // x the grid's lanes from the end: finer claims (0: 64-sample chunks throughout)
@@ -379,6 +382,13 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     // the trapped lane advances one bounce per walk instead of one per shared
     // shading step (the frame cannot end before it does).
     bool long_walk = false;
+#if BDPT_HELP
+    // helping: the lane walks a task's shadow ray (tracing is set too; its ring slot in rt)
+    bool helping = false;
+    if (lane0()) task_ctl()[0] = task_ctl()[1] = 0u;
+#else
+    constexpr bool helping = false;
+#endif
 #if BDPT_COOP_ALONE
     bool coop_wait = false;  // a closest-hit walk begun, waiting for its turn to be walked by the whole wave
 #endif
@@ -415,7 +425,8 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // samples (mt_x397) runs once with every lane busy, instead of once per
         // refill with only the refilled lanes doing useful work.
         while (!exhausted && !express) {
-            const uint64_t idle = __ballot(L.state == ST_IDLE);
+            const bool refill = L.state == ST_IDLE && !(BDPT_HELP && helping);  // (a helper's L.ray is its task's)
+            const uint64_t idle = __ballot(refill);
             if (!idle) break;
             if (chunk_pos >= chunk_n) {
                 if (global_done) {
@@ -461,7 +472,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const int m = min(popc64(idle), chunk_n - chunk_pos);
             const int rank = lanes_below(idle);
             const uint32_t x397 = __shfl(chunk_x397, (chunk_pos + rank) & 63);
-            if (L.state == ST_IDLE && rank < m) start_sample<true>(L, chunk_base + chunk_pos + rank, P->fr, x397);
+            if (refill && rank < m) start_sample<true>(L, chunk_base + chunk_pos + rank, P->fr, x397);
             chunk_pos += m;
         }
 #else
@@ -481,7 +492,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             }
         }
 #endif
+#if BDPT_HELP
+        // the wave ends only with its task ring drained and no helper walking
+        if (__ballot(BDPT_BUSY(L.state) || helping) == 0 && task_ctl()[0] == task_ctl()[1]) {
+#else
         if (__ballot(BDPT_BUSY(L.state)) == 0) {
+#endif
             if (exhausted) break;
             continue;
         }
@@ -685,6 +701,60 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         const int steady_ready = P->fr.shade_ready > 0 ? P->fr.shade_ready : BDPT_SHADE_READY;
 #endif
         for (;;) {  // walk until enough lanes have a result to shade
+#if BDPT_HELP
+            uint64_t tr = __ballot(tracing);
+            const uint64_t ready = __ballot(has_res && !tracing);  // helpers shade after their walk
+            if (popc64(ready) >= (BDPT_TAIL_SHADE == 1 && exhausted ? 1
+                                  : BDPT_TAIL_SHADE == 2 && exhausted ? max(1, (popc64(tr | ready) * BDPT_TAIL_FRAC) >> 3)
+                                                                      : steady_ready))
+                break;
+            // Lanes that wait (a result kept, or no sample) claim the ring's oldest
+            // tasks, one each, and walk their shadow rays with the walk code below.
+            bool hfin = false;  // a helper walk that ended in this iteration (result in ts.best)
+            {
+                lds_u32* const ctl = task_ctl();
+                const uint32_t head = ctl[0], tail = ctl[1];
+                const bool cand = !tracing && (has_res || L.state == ST_IDLE);
+                const uint64_t cm = head != tail ? __ballot(cand) : 0ull;
+                if (cm) {
+                    const uint32_t n = min(static_cast<uint32_t>(popc64(cm)), tail - head);
+                    const uint32_t rank = static_cast<uint32_t>(lanes_below(cm));
+                    ctl[0] = head + n;
+                    if (cand && rank < n) {
+                        if (has_res) help_compact(L, res, rt, ru, rv, P->sc);  // frees L.ray
+                        const uint32_t slot = (head + rank) & (P->fr.task_cap - 1);
+                        const float4* const q = task_ring(P->fr) + 3 * static_cast<size_t>(slot);
+                        const float4 a = gld4(q), b = gld4(q + 1);
+                        L.ray = Ray{xyz(a), xyz(b), kEpsilon, a.w};
+                        rt = __uint_as_float(slot);
+                        q_any = true;
+                        helping = true;
+                        if (COUNT) cnt.c[1]++;
+                        ri = ray_inv(L.ray, b.w);
+                        ts.best = -1;
+                        if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root: unoccluded
+                            hfin = true;
+                        } else if (!ri.fast || far_origin(P->sc, L.ray.o)) {  // the reference's tree, unculled
+                            const TravResult qr = traverse_binary<COUNT, Stack>(P->sc, L.ray, true, false, stk);
+                            if (COUNT) cnt.c[2] += qr.nodes, cnt.c[3] += qr.tris, cnt.c[15] += qr.exact;
+                            ts.best = qr.best;
+                            hfin = true;
+                        } else {
+                            ts = trav_begin(tsc, L.ray);
+                            tracing = true;
+#if BDPT_ROOT_LDS
+                            if (root_in_lds && !walk_begin_lds<COUNT, SLACK>(root_lds, L.ray, ri, true, ts, stk, cnt)) {
+                                tracing = false;  // no child hit: unoccluded
+                                hfin = true;
+                            }
+#endif
+                        }
+                    }
+                }
+            }
+            tr = __ballot(tracing);
+            if (!tr && !__ballot(hfin)) break;
+#else
             const uint64_t tr = __ballot(tracing);
             if (!tr) break;
             const uint64_t ready = __ballot(has_res);
@@ -697,6 +767,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                                                                         : (P->fr.shade_ready > 0 ? P->fr.shade_ready : BDPT_SHADE_READY)))
 #endif
                 break;
+#endif
 #if BDPT_TRAV_SPLIT
             // Lanes at a leaf and lanes at an interior node step in alternate
             // iterations (whichever group is larger in the sense of the ratio
@@ -714,14 +785,41 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #else
             if (tracing && trav_step<COUNT, SLACK>(tsc, L.ray, ri, q_any, ts, stk, cnt)) {
 #endif
+#if BDPT_HELP
+                tracing = false;
+                if (helping) {
+                    hfin = true;
+                } else {
+                    res = ts.best, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;
+                    has_res = true;
+                }
+#else
                 res = ts.best, rt = ts.best_t, ru = ts.best_u, rv = ts.best_v;
                 tracing = false;
                 has_res = true;
+#endif
             }
+#if BDPT_HELP
+            if (hfin) {  // the task's shadow ray: unoccluded -> its contribution to the pixel
+                helping = false;
+                if (ts.best < 0) {
+                    const float4 c = gld4(task_ring(P->fr) + 3 * static_cast<size_t>(__float_as_uint(rt)) + 2);
+                    const uint32_t meta = __float_as_uint(c.w);
+                    const int px = static_cast<int>(meta & kTaskPixel);
+                    if (meta & kTaskSplat) {
+                        if (COUNT) cnt.c[6]++;
+                        splat_add(P->fb, px, xyz(c));
+                    } else {
+                        eye_add(P->fb, px, xyz(c));
+                    }
+                }
+            }
+#endif
         }
         const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
-        const bool shading = COUNT && __ballot(has_res) != 0;
-        if (has_res) {
+        const bool shade_now = has_res && !(BDPT_HELP && tracing);  // (a helper mid-walk shades next time)
+        const bool shading = COUNT && __ballot(shade_now) != 0;
+        if (shade_now) {
             has_res = false;
 #if BDPT_DEEP_RNG && BDPT_RING_AHEAD
             // the draws of this step past 227 are read from the ring: generate them first

@@ -312,6 +312,80 @@ __device__ __forceinline__ void eye_slot_reset(float* __restrict__ fb, int k, in
 }
 #endif
 
+// Shadow-ray tasks (BDPT_HELP, the frame kernels without Russian roulette; round 6,
+// VERDICT r5 item 1). The wave's owners hold ~99 connection tasks per shading step,
+// and serialising them through each owner's one query per step kept both the
+// shading steps (one per connection) and the walk loop's lane occupancy (waiting
+// lanes idle) low. Here an owner computes every connection of a vertex at once —
+// connectToCamera's splat (bdpt.h:295-371), connectToLight (bdpt.h:374-430) and
+// connectVertices with all light vertices (bdpt.h:434-483), everything but the
+// visibility test, in the reference's order and arithmetic — and pushes each
+// shadow ray with its contribution (already scaled by 1 / spp for the eye
+// estimate) and target pixel into its wave's ring, then continues its walk in the
+// same shading step. Lanes of the wave that wait in the walk loop (their own
+// result ready, or no sample) claim tasks and walk them; an unoccluded one adds its
+// contribution to the pixel (the wave's eye slot, else the framebuffer). The
+// visibility tests and contributions are the reference's; only the order of the
+// float additions into a pixel changes (as with the device atomics). A full ring
+// makes the owner trace that shadow ray itself, as the serial build does.
+#ifndef BDPT_HELP
+#define BDPT_HELP 0
+#endif
+#if BDPT_HELP && !BDPT_SAMPLER_STATE
+constexpr uint32_t kTaskSplat = 0x40000000u;   // meta bit: a camera splat (framebuffer add, bdpt.h:363-370)
+constexpr uint32_t kTaskPixel = 0x3fffffffu;
+constexpr int kResShaded = -2;  // an own closest-hit result already applied to the lane (walk loop, help_compact)
+__shared__ uint32_t g_task_ctl[4][2];  // per wave of the block: ring head (claimed), tail (pushed)
+__device__ __forceinline__ lds_u32* task_ctl() { return (lds_u32*)g_task_ctl[(opaque_tid() >> 6) & 3]; }
+__device__ __forceinline__ float4* task_ring(const DevFrame& fr) {
+    const uint32_t wave = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * 4 + (threadIdx.x >> 6))));
+    return fr.tasks + static_cast<size_t>(wave) * fr.task_cap * 3;
+}
+// Called by the lanes that push (their exec mask is the set): true if this lane's
+// task went into the ring (false: the ring is full; the caller traces it itself).
+__device__ __forceinline__ bool task_push(const DevFrame& fr, const Ray& r, bool nocull, f3 c, int pixel, bool splat) {
+    lds_u32* const ctl = task_ctl();
+    const uint64_t m = __ballot(true);
+    const uint32_t head = ctl[0], tail = ctl[1];
+    const uint32_t n = static_cast<uint32_t>(popc64(m)), rank = static_cast<uint32_t>(lanes_below(m));
+    const uint32_t space = fr.task_cap - (tail - head);
+    const uint32_t k = n < space ? n : space;
+    ctl[1] = tail + k;  // (every pushing lane writes the same value)
+    if (rank >= k) return false;
+    float4* const q = task_ring(fr) + 3 * static_cast<size_t>((tail + rank) & (fr.task_cap - 1));
+    // (o, max_t) (d, near cull) (contribution, pixel | splat bit): the claim reads the first two
+    gst4(q, make_float4(r.o.x, r.o.y, r.o.z, r.max_t));
+    gst4(q + 1, make_float4(r.d.x, r.d.y, r.d.z, nocull ? kNoCullNear : kCullNear));
+    gst4(q + 2, make_float4(c.x, c.y, c.z, __uint_as_float(static_cast<uint32_t>(pixel) | (splat ? kTaskSplat : 0u))));
+    return true;
+}
+#else
+constexpr int kResShaded = -2;
+__device__ __forceinline__ bool task_push(const DevFrame&, const Ray&, bool, f3, int, bool) { return false; }
+#endif
+constexpr bool kTasks = BDPT_HELP && !BDPT_SAMPLER_STATE;
+
+// An eye-estimate addition for the pixel: the wave's slot when it holds the pixel, else the framebuffer.
+__device__ __forceinline__ void eye_add(float* __restrict__ fb, int pixel, f3 add) {
+#if BDPT_EYE_SLOTS && !BDPT_SAMPLER_STATE
+    float4* const s = wave_eye_slots();
+    int k = -1;
+#pragma unroll
+    for (int j = 0; j < BDPT_EYE_SLOTS; j++)
+        if (__float_as_int(s[j].w) == pixel) k = j;
+    if (k >= 0) {
+        atomicAdd(&s[k].x, add.x);
+        atomicAdd(&s[k].y, add.y);
+        atomicAdd(&s[k].z, add.z);
+        return;
+    }
+#endif
+    float* px = fb + 3 * static_cast<size_t>(pixel);
+    gadd(px + 0, add.x);
+    gadd(px + 1, add.y);
+    gadd(px + 2, add.z);
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __restrict__ fb, Counts& cnt) {
     if (COUNT) {
@@ -322,25 +396,7 @@ __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __res
     // rgb[p] += acc * (1 / spp) (renderer.cpp:202), one sample at a time.
     if (!(fr.flags & kFlagNoEyeAccum) && (L.c.Li.x != 0.f || L.c.Li.y != 0.f || L.c.Li.z != 0.f)) {
         const float inv_spp = fr.inv_spp;  // 1.f / spp
-        const f3 add = L.c.Li * inv_spp;
-#if BDPT_EYE_SLOTS && !BDPT_SAMPLER_STATE
-        float4* const s = wave_eye_slots();
-        int k = -1;
-#pragma unroll
-        for (int j = 0; j < BDPT_EYE_SLOTS; j++)
-            if (__float_as_int(s[j].w) == L.c.pixel) k = j;
-        if (k >= 0) {
-            atomicAdd(&s[k].x, add.x);
-            atomicAdd(&s[k].y, add.y);
-            atomicAdd(&s[k].z, add.z);
-        } else
-#endif
-        {
-            float* px = fb + 3 * static_cast<size_t>(L.c.pixel);
-            gadd(px + 0, add.x);
-            gadd(px + 1, add.y);
-            gadd(px + 2, add.z);
-        }
+        eye_add(fb, L.c.pixel, L.c.Li * inv_spp);
     }
     L.state = ST_IDLE;
 }
@@ -400,6 +456,10 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
     return true;
 }
 
+// cull_near_for's rule for a shadow ray in direction d leaving the lane's current
+// vertex (NEE, connectVertices): true = no near cull.
+__device__ __forceinline__ bool vertex_nocull(const Lane& L, f3 d);
+
 // BDPT_GRAZE_IN_DIST 1: a vertex's near-cull threshold (graze_threshold) is
 // decoded once, in its vertex body, into Hit::dist (dead after that body), and
 // the queries leaving the vertex compare against it (cull_near_for).
@@ -455,9 +515,13 @@ __device__ __forceinline__ bool walk_continues(Lane& L, const DevFrame& fr) {
         const float prevRev = ep.rev * (rr_on(fr) ? L.c.rr : 1.f);  /* swapped (wi, wo) * lightVertex.rr (bdpt.h:342) */ \
         const float lightWeight = div_w(reversePdf_a, nlight) * (L.c.vcm + prevRev * L.c.vc); \
         const float mis = rcp_w(lightWeight + 1.f + 0.f); \
-        L.c.pend = (fr.strategy == 0) ? rad * mis : rad; \
-        L.c.pend_px = yp * fr.W + xp; \
-        L.ray = shadow_ray(cam_o, L.h.p); \
+        const f3 pend_ = (fr.strategy == 0) ? rad * mis : rad; \
+        const int px_ = yp * fr.W + xp; \
+        const Ray sr_ = shadow_ray(cam_o, L.h.p); \
+        if (kTasks && task_push(fr, sr_, false, pend_, px_, true)) break;  /* a helper walks it (act: A_LIGHT_CONTINUE) */ \
+        L.c.pend = pend_; \
+        L.c.pend_px = px_; \
+        L.ray = sr_; \
         L.state = ST_SPLAT; \
         act = A_ISSUED; \
     } BDPT_END;
@@ -658,8 +722,12 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const float eyeCurRev_a = cosAtEye * rcp_w(d2) * kInvTwoPi;
         const float eyeWeight = eyeCurRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
         const float mis = rcp_w(lightWeight + 1.f + eyeWeight);
-        L.c.pend = (fr.strategy == 0) ? Li * mis : Li;
-        L.ray = shadow_ray(L.h.p, e_p);
+        const f3 pend = (fr.strategy == 0) ? Li * mis : Li;
+        const Ray sr = shadow_ray(L.h.p, e_p);
+        if (kTasks && task_push(fr, sr, vertex_nocull(L, sr.d), pend * fr.inv_spp, L.c.pixel, false))
+            break;  // a helper walks it (act: A_CONN)
+        L.c.pend = pend;
+        L.ray = sr;
         L.state = ST_NEE;
         act = A_ISSUED;
     } BDPT_END;
@@ -710,8 +778,13 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
             const float eyeWeight = eyePathRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
             const float mis = rcp_w(lightWeight + 1.f + eyeWeight);
+            const Ray sr = shadow_ray(L.h.p, V.p);
+            if (kTasks && task_push(fr, sr, vertex_nocull(L, sr.d), (Li * mis) * fr.inv_spp, L.c.pixel, false)) {
+                L.c.ci++;  // a helper walks it; the next light vertex now
+                continue;
+            }
             L.c.pend = Li * mis;
-            L.ray = shadow_ray(L.h.p, V.p);
+            L.ray = sr;
             L.state = ST_CONN;
             act = A_ISSUED;
             break;
@@ -775,6 +848,13 @@ __device__ __forceinline__ bool is_shadow_state(uint32_t st) { return st == ST_S
 // bdpt_device.hpp): none for a query that leaves the current vertex (or, for the
 // first light-subpath ray, the emitter: A_START_LIGHT puts its normal and face
 // code in L.h) nearly parallel to its triangle's plane; camera queries keep it.
+__device__ __forceinline__ bool vertex_nocull(const Lane& L, f3 d) {
+#if BDPT_GRAZE_IN_DIST
+    return fabsf(dot(d, L.h.n)) < L.h.dist;
+#else
+    return graze_exempt(d, L.h.n, L.h.shape);
+#endif
+}
 __device__ __forceinline__ float cull_near_for(const Lane& L) {
     const uint32_t st = L.state;
     if (st == ST_PRIMARY || st == ST_SPLAT) return kCullNear;
@@ -792,18 +872,21 @@ template <bool COUNT>
 __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, float v, const DevScene& sc,
                                             const DevFrame& fr, float* __restrict__ fb, Counts& cnt) {
     const bool any = is_shadow_state(L.state);
-    bool hit = res >= 0;
-    if (hit && !any) hit = (t <= L.ray.max_t && t >= L.ray.min_t);  // accel.h:133
+    const bool shaded = kTasks && res == kResShaded;  // applied in the walk loop already (help_compact)
+    bool hit = res >= 0 || shaded;
+    if (hit && !any && !shaded) hit = (t <= L.ray.max_t && t >= L.ray.min_t);  // accel.h:133
     // The primary hit is shaded later, by the eye walk's first vertex (A_START_EYE
     // keeps its (t, u, v)); the light walk overwrites L.h before reading it.
-    if (hit && !any && L.state != ST_PRIMARY) shade_hit(sc, res, u, v, t, L.ray.d, L.h);
+    if (hit && !any && !shaded && L.state != ST_PRIMARY) shade_hit(sc, res, u, v, t, L.ray.d, L.h);
     uint32_t act;
     switch (L.state) {
         case ST_PRIMARY:
             if (!hit) act = A_FINISH;
             else {
-                L.c.prim_tri = res;
-                L.c.Li = mk(t, u, v);
+                if (!shaded) {
+                    L.c.prim_tri = res;
+                    L.c.Li = mk(t, u, v);
+                }
                 act = (fr.strategy == 2) ? A_START_EYE : A_START_LIGHT;
             }
             break;
@@ -831,6 +914,26 @@ __device__ __forceinline__ uint32_t resolve(Lane& L, int res, float t, float u, 
     // A state-machine bug must not hang the GPU: bound the queries per sample.
     if (++L.c.steps > (rr_on(fr) ? (1 << 30) : max_steps_per_sample(fr.rr_depth)) && act != A_FINISH) act = A_FINISH;
     return act;
+}
+
+// BDPT_HELP: an own closest-hit result applied where resolve() would apply it
+// (accel.h:133's range test, the primary hit's (t, u, v) into the cold state, or
+// the hit shaded into L.h), so the lane's ray registers are free for a helper walk;
+// res becomes kResShaded (a hit) or -1 (a miss).
+__device__ __forceinline__ void help_compact(Lane& L, int& res, float t, float u, float v, const DevScene& sc) {
+    const uint32_t st = L.state;
+    if (res < 0 || !(st == ST_PRIMARY || st == ST_LIGHT || st == ST_EYE)) return;
+    if (!(t <= L.ray.max_t && t >= L.ray.min_t)) {
+        res = -1;
+        return;
+    }
+    if (st == ST_PRIMARY) {
+        L.c.prim_tri = res;
+        L.c.Li = mk(t, u, v);
+    } else {
+        shade_hit(sc, res, u, v, t, L.ray.d, L.h);
+    }
+    res = kResShaded;
 }
 
 // Schedules without an overlapped walk run a deferred action at once.
