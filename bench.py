@@ -413,6 +413,8 @@ def main() -> None:
                 "bytes_per_sample_layout_model": round(bps_layout, 1),
                 "achieved_layout_model": round(bps_layout * local_samples / kernel_s / 1e9, 2),
                 "counts_per_sample": {k: round(v / cst["samples"], 3) for k, v in cts.items()},
+                # the counting pass's schedule counters (bdpt_stats.sched; Counts::q), per sample
+                "sched_per_sample": {k: round(v / cst["samples"], 4) for k, v in cst["sched"].items()},
                 # the persistent grid's end tail (device clock: the frame's last 64-sample chunk
                 # claimed -> last wave done), what a 1/N row shard pays again per rank
                 "tail_ms": round(sum(tail_ms) / max(len(tail_ms), 1), 3)}

@@ -869,7 +869,9 @@ struct Counts {
     // connection-task histogram of the shading steps (frame kernels' counting pass): the
     // tasks a wave holds when it shades — connectVertices still to run (nl - ci at A_CONN),
     // connectToLight + all connections of a new eye vertex, connectToCamera of a new light
-    // vertex — summed over steps, the steps, steps with >= 32 and >= 64 tasks
+    // vertex — summed over steps, the steps, steps with >= 32 and >= 64 tasks. The
+    // BDPT_HELP builds count their task rings here instead: tasks pushed, pushes
+    // refused (ring full: the owner traces the ray), claim rounds, tasks claimed.
     uint32_t q[4];
     uint32_t t_step;  // this lane's tasks in the current shading step
 };

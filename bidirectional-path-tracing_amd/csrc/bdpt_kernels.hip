@@ -288,6 +288,16 @@ struct KParams {
 #ifndef BDPT_COOP_GROUPS
 #define BDPT_COOP_GROUPS 1  // express waves with 2-4 long walks walk them at once in groups of 32 / 16 lanes (coop_closest_groups; RR Caustic frames 42.7-45.2 s vs 43.8-54.0)
 #endif
+#ifndef BDPT_HELP_BATCH
+#define BDPT_HELP_BATCH 0  // BDPT_HELP: the shading step's connections flattened over the wave (conn_batch)
+#endif
+#if !BDPT_HELP
+#undef BDPT_HELP_BATCH
+#define BDPT_HELP_BATCH 0
+#endif
+#ifndef BDPT_HELP_MIN
+#define BDPT_HELP_MIN 1  // BDPT_HELP: fewest waiting lanes that start a claim round (unless the ring holds fewer tasks)
+#endif
 #ifndef BDPT_TAIL_PROBE
 #define BDPT_TAIL_PROBE 0  // measurement only (non-RR builds): the drain phase in the RR diag words (tools/tail_probe.py)
 #endif
@@ -385,7 +395,10 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #if BDPT_HELP
     // helping: the lane walks a task's shadow ray (tracing is set too; its ring slot in rt)
     bool helping = false;
-    if (lane0()) task_ctl()[0] = task_ctl()[1] = 0u;
+    {
+        const TaskCtl ctl = task_ctl(L.c);
+        if (lane0()) *ctl.head = *ctl.tail = 0u;
+    }
 #else
     constexpr bool helping = false;
 #endif
@@ -494,7 +507,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
 #if BDPT_HELP
         // the wave ends only with its task ring drained and no helper walking
-        if (__ballot(BDPT_BUSY(L.state) || helping) == 0 && task_ctl()[0] == task_ctl()[1]) {
+        if (__ballot(BDPT_BUSY(L.state) || helping) == 0 && *task_ctl(L.c).head == *task_ctl(L.c).tail) {
 #else
         if (__ballot(BDPT_BUSY(L.state)) == 0) {
 #endif
@@ -712,21 +725,33 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             // tasks, one each, and walk their shadow rays with the walk code below.
             bool hfin = false;  // a helper walk that ended in this iteration (result in ts.best)
             {
-                lds_u32* const ctl = task_ctl();
-                const uint32_t head = ctl[0], tail = ctl[1];
-                const bool cand = !tracing && (has_res || L.state == ST_IDLE);
-                const uint64_t cm = head != tail ? __ballot(cand) : 0ull;
+                const TaskCtl ctl = task_ctl(L.c);
+                const uint32_t head = *ctl.head, tail = *ctl.tail;
+                // (a lane waiting on its own shadow ray, pushed by itself when the ring was
+                // full, keeps its pending contribution in L.c.pend: it does not help)
+                const bool cand = !tracing && (has_res ? !is_shadow_state(L.state) : L.state == ST_IDLE);
+                uint64_t cm = head != tail ? __ballot(cand) : 0ull;
+                // claim rounds only with enough takers (each round exposes one record load):
+                // BDPT_HELP_MIN lanes, or any once the wave's own walks have ended
+                if (popc64(cm) < BDPT_HELP_MIN && popc64(cm) < static_cast<int>(tail - head) && __ballot(tracing)) cm = 0;
                 if (cm) {
+                    if (COUNT && lane0()) cnt.q[2]++;  // (counting pass: claim rounds)
                     const uint32_t n = min(static_cast<uint32_t>(popc64(cm)), tail - head);
                     const uint32_t rank = static_cast<uint32_t>(lanes_below(cm));
-                    ctl[0] = head + n;
+                    *ctl.head = head + n;
                     if (cand && rank < n) {
                         if (has_res) help_compact(L, res, rt, ru, rv, P->sc);  // frees L.ray
                         const uint32_t slot = (head + rank) & (P->fr.task_cap - 1);
-                        const float4* const q = task_ring(P->fr) + 3 * static_cast<size_t>(slot);
-                        const float4 a = gld4(q), b = gld4(q + 1);
+                        float4* const ring = task_ring(P->fr);
+                        const uint32_t cap = P->fr.task_cap;
+                        const float4 a = gld4(task_vec(ring, cap, slot, 0)), b = gld4(task_vec(ring, cap, slot, 1)),
+                                     c = gld4(task_vec(ring, cap, slot, 2));
+                        if (COUNT) cnt.q[3]++;  // (counting pass: claims)
                         L.ray = Ray{xyz(a), xyz(b), kEpsilon, a.w};
-                        rt = __uint_as_float(slot);
+                        // the contribution and pixel into the lane's (free) pending-connection
+                        // fields: the slot may be pushed over once claimed
+                        L.c.pend = xyz(c);
+                        L.c.pend_px = __float_as_int(c.w);
                         q_any = true;
                         helping = true;
                         if (COUNT) cnt.c[1]++;
@@ -803,14 +828,13 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             if (hfin) {  // the task's shadow ray: unoccluded -> its contribution to the pixel
                 helping = false;
                 if (ts.best < 0) {
-                    const float4 c = gld4(task_ring(P->fr) + 3 * static_cast<size_t>(__float_as_uint(rt)) + 2);
-                    const uint32_t meta = __float_as_uint(c.w);
+                    const uint32_t meta = static_cast<uint32_t>(L.c.pend_px);
                     const int px = static_cast<int>(meta & kTaskPixel);
                     if (meta & kTaskSplat) {
                         if (COUNT) cnt.c[6]++;
-                        splat_add(P->fb, px, xyz(c));
+                        splat_add(P->fb, px, L.c.pend);
                     } else {
-                        eye_add(P->fb, px, xyz(c));
+                        eye_add(P->fb, px, L.c.pend);
                     }
                 }
             }
@@ -818,6 +842,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         }
         const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
         const bool shade_now = has_res && !(BDPT_HELP && tracing);  // (a helper mid-walk shades next time)
+#if BDPT_HELP_BATCH
+        uint32_t act2 = A_DONE;
+#endif
         const bool shading = COUNT && __ballot(shade_now) != 0;
         if (shade_now) {
             has_res = false;
@@ -829,15 +856,26 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             const uint64_t r0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
             const uint32_t act = resolve<COUNT>(L, res, rt, ru, rv, P->sc, P->fr, P->fb, cnt);
             if (COUNT && first_active_lane()) cnt.c[20] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - r0);
+#if BDPT_HELP_BATCH
+            act2 = advance<COUNT, 1>(L, act, P->sc, P->fr, P->fb, ls, cnt);
+#else
             advance<COUNT>(L, act, P->sc, P->fr, P->fb, ls, cnt);
+#endif
             if (BDPT_RR == 1) long_walk = L.state != ST_IDLE && L.c.depth > P->fr.express_depth;
         }
+#if BDPT_HELP_BATCH
+        // the connections of the eye vertices reached in this step, over the whole wave
+        if (__ballot(shade_now)) {
+            conn_batch<COUNT>(L, shade_now && act2 == A_CONN && P->fr.strategy == 0, P->sc, P->fr, ls, cnt);
+            if (shade_now) advance<COUNT, 2>(L, act2, P->sc, P->fr, P->fb, ls, cnt);
+        }
+#endif
         if (COUNT && first_active_lane()) {
             const uint64_t c2 = __builtin_amdgcn_s_memtime();
             cnt.c[12] += static_cast<uint32_t>(c1 - c0);
             cnt.c[13] += static_cast<uint32_t>(c2 - c1);
         }
-        if (COUNT && shading) {  // the connection tasks the wave held in this shading step (Counts::q)
+        if (COUNT && shading && !BDPT_HELP) {  // the connection tasks the wave held in this shading step (Counts::q)
             uint32_t tw = cnt.t_step;
             for (int off = 32; off > 0; off >>= 1) tw += static_cast<uint32_t>(__shfl_xor(static_cast<int>(tw), off));
             cnt.t_step = 0;

@@ -64,6 +64,10 @@ struct LightStore {
         const uint32_t s = tid_rel ? slot + opaque_tid() : slot;
         return base + (static_cast<size_t>(s) * maxv + static_cast<uint32_t>(v)) * 4;
     }
+    // vertex v of the lane threadIdx.x == tid (tid_rel stores only)
+    __device__ __forceinline__ float4* at_tid(int v, uint32_t tid) const {
+        return base + (static_cast<size_t>(slot + tid) * maxv + static_cast<uint32_t>(v)) * 4;
+    }
 };
 __device__ __forceinline__ LightStore light_store(float* lv, int lv_max, uint32_t slot) {
     return LightStore{reinterpret_cast<float4*>(lv), static_cast<uint32_t>(lv_max > 1 ? lv_max : 1), slot};
@@ -106,6 +110,15 @@ __device__ __forceinline__ void store_vertex(const LightStore& ls, int v, const 
     lv_st(q + 3, make_float4(tp.x, tp.y, tp.z, __int_as_float(h.mat)));
 }
 
+__device__ __forceinline__ Vertex load_vertex_at(const float4* q) {
+    const float4 a = lv_ld(q), b = lv_ld(q + 1), c = lv_ld(q + 2), d = lv_ld(q + 3);
+    Vertex x;
+    x.p = xyz(a), x.vcm = a.w;
+    x.n = xyz(b), x.vc = b.w;
+    x.wo = xyz(c), x.rr = c.w;
+    x.tp = xyz(d), x.mat = __float_as_int(d.w);
+    return x;
+}
 __device__ __forceinline__ Vertex load_vertex(const LightStore& ls, int v) {
     const float4* q = ls.at(v);
     const float4 a = lv_ld(q), b = lv_ld(q + 1), c = lv_ld(q + 2), d = lv_ld(q + 3);
@@ -335,33 +348,56 @@ __device__ __forceinline__ void eye_slot_reset(float* __restrict__ fb, int k, in
 constexpr uint32_t kTaskSplat = 0x40000000u;   // meta bit: a camera splat (framebuffer add, bdpt.h:363-370)
 constexpr uint32_t kTaskPixel = 0x3fffffffu;
 constexpr int kResShaded = -2;  // an own closest-hit result already applied to the lane (walk loop, help_compact)
-__shared__ uint32_t g_task_ctl[4][2];  // per wave of the block: ring head (claimed), tail (pushed)
-__device__ __forceinline__ lds_u32* task_ctl() { return (lds_u32*)g_task_ctl[(opaque_tid() >> 6) & 3]; }
+// The wave's ring positions live in LDS, in the Russian-roulette field of its
+// first two lanes' cold records (unused by these builds; the LDS of 4 resident
+// blocks is full): head (tasks claimed) in lane 0's, tail (pushed) in lane 1's.
+struct TaskCtl {
+    lds_u32* head;
+    lds_u32* tail;
+};
+__device__ __forceinline__ TaskCtl task_ctl(const LaneCold& mine) {
+    lds_u32* const w = (lds_u32*)(&mine - (opaque_tid() & 63));
+    constexpr uint32_t kRrWord = offsetof(LaneCold, rr) / 4, kStride = sizeof(LaneCold) / 4;
+    return TaskCtl{w + kRrWord, w + kStride + kRrWord};
+}
 __device__ __forceinline__ float4* task_ring(const DevFrame& fr) {
     const uint32_t wave = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * 4 + (threadIdx.x >> 6))));
     return fr.tasks + static_cast<size_t>(wave) * fr.task_cap * 3;
 }
 // Called by the lanes that push (their exec mask is the set): true if this lane's
 // task went into the ring (false: the ring is full; the caller traces it itself).
-__device__ __forceinline__ bool task_push(const DevFrame& fr, const Ray& r, bool nocull, f3 c, int pixel, bool splat) {
-    lds_u32* const ctl = task_ctl();
+#ifndef BDPT_HELP_SOA
+#define BDPT_HELP_SOA 1  // the ring as three planes of 16-byte vectors (consecutive slots' pushes and claims coalesce)
+#endif
+// float4 k (0..2) of ring slot `slot`
+__device__ __forceinline__ float4* task_vec(float4* ring, uint32_t cap, uint32_t slot, int k) {
+    return BDPT_HELP_SOA ? ring + static_cast<size_t>(k) * cap + slot : ring + 3 * static_cast<size_t>(slot) + k;
+}
+__device__ __forceinline__ bool task_push(const LaneCold& mine, const DevFrame& fr, const Ray& r, bool nocull, f3 c,
+                                          int pixel, bool splat, Counts& cnt) {
+    const TaskCtl ctl = task_ctl(mine);
     const uint64_t m = __ballot(true);
-    const uint32_t head = ctl[0], tail = ctl[1];
+    const uint32_t head = *ctl.head, tail = *ctl.tail;
     const uint32_t n = static_cast<uint32_t>(popc64(m)), rank = static_cast<uint32_t>(lanes_below(m));
     const uint32_t space = fr.task_cap - (tail - head);
     const uint32_t k = n < space ? n : space;
-    ctl[1] = tail + k;  // (every pushing lane writes the same value)
+    *ctl.tail = tail + k;  // (every pushing lane writes the same value)
+    cnt.q[rank < k ? 0 : 1]++;  // (counting pass: pushed / refused)
     if (rank >= k) return false;
-    float4* const q = task_ring(fr) + 3 * static_cast<size_t>((tail + rank) & (fr.task_cap - 1));
-    // (o, max_t) (d, near cull) (contribution, pixel | splat bit): the claim reads the first two
-    gst4(q, make_float4(r.o.x, r.o.y, r.o.z, r.max_t));
-    gst4(q + 1, make_float4(r.d.x, r.d.y, r.d.z, nocull ? kNoCullNear : kCullNear));
-    gst4(q + 2, make_float4(c.x, c.y, c.z, __uint_as_float(static_cast<uint32_t>(pixel) | (splat ? kTaskSplat : 0u))));
+    float4* const ring = task_ring(fr);
+    const uint32_t slot = (tail + rank) & (fr.task_cap - 1);
+    // (o, max_t) (d, near cull) (contribution, pixel | splat bit)
+    gst4(task_vec(ring, fr.task_cap, slot, 0), make_float4(r.o.x, r.o.y, r.o.z, r.max_t));
+    gst4(task_vec(ring, fr.task_cap, slot, 1), make_float4(r.d.x, r.d.y, r.d.z, nocull ? kNoCullNear : kCullNear));
+    gst4(task_vec(ring, fr.task_cap, slot, 2),
+         make_float4(c.x, c.y, c.z, __uint_as_float(static_cast<uint32_t>(pixel) | (splat ? kTaskSplat : 0u))));
     return true;
 }
 #else
 constexpr int kResShaded = -2;
-__device__ __forceinline__ bool task_push(const DevFrame&, const Ray&, bool, f3, int, bool) { return false; }
+__device__ __forceinline__ bool task_push(const LaneCold&, const DevFrame&, const Ray&, bool, f3, int, bool, Counts&) {
+    return false;
+}
 #endif
 constexpr bool kTasks = BDPT_HELP && !BDPT_SAMPLER_STATE;
 
@@ -518,7 +554,7 @@ __device__ __forceinline__ bool vertex_nocull(const Lane& L, f3 d);
         const f3 pend_ = (fr.strategy == 0) ? rad * mis : rad; \
         const int px_ = yp * fr.W + xp; \
         const Ray sr_ = shadow_ray(cam_o, L.h.p); \
-        if (kTasks && task_push(fr, sr_, false, pend_, px_, true)) break;  /* a helper walks it (act: A_LIGHT_CONTINUE) */ \
+        if (kTasks && task_push(L.c, fr, sr_, false, pend_, px_, true, cnt)) break;  /* a helper walks it (act: A_LIGHT_CONTINUE) */ \
         L.c.pend = pend_; \
         L.c.pend_px = px_; \
         L.ray = sr_; \
@@ -572,12 +608,16 @@ __device__ __forceinline__ bool vertex_nocull(const Lane& L, f3 d);
         } \
     } BDPT_END;
 
-template <bool COUNT>
-__device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
-                        const LightStore& ls, Counts& cnt) {
+// PART 0: the whole sweep; 1: the bodies before connectVertices, returning the
+// action reached; 2: connectVertices and the bodies after it (the BDPT_HELP_BATCH
+// schedule runs the wave's connections between the two, conn_batch).
+template <bool COUNT, int PART = 0>
+__device__ uint32_t advance(Lane& L, uint32_t act, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
+                            const LightStore& ls, Counts& cnt) {
     const f3 cam_o = mk(fr.cam_o[0], fr.cam_o[1], fr.cam_o[2]);
     const f3 fwd = mk(fr.cam.fwd[0], fr.cam.fwd[1], fr.cam.fwd[2]);
-    if (COUNT && act == A_CONN && fr.strategy == 0) cnt.t_step += static_cast<uint32_t>(L.c.nl - L.c.ci);  // (Counts::q)
+    if (COUNT && PART != 2 && act == A_CONN && fr.strategy == 0) cnt.t_step += static_cast<uint32_t>(L.c.nl - L.c.ci);  // (Counts::q)
+    if (PART != 2) {
 #if BDPT_SPLIT_CONTINUE
     BDPT_BODY_LIGHT_VERTEX
     BDPT_BODY_CONTINUE(A_LIGHT_CONTINUE, act == A_LIGHT_CONTINUE)
@@ -724,7 +764,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         const float mis = rcp_w(lightWeight + 1.f + eyeWeight);
         const f3 pend = (fr.strategy == 0) ? Li * mis : Li;
         const Ray sr = shadow_ray(L.h.p, e_p);
-        if (kTasks && task_push(fr, sr, vertex_nocull(L, sr.d), pend * fr.inv_spp, L.c.pixel, false))
+        if (kTasks && task_push(L.c, fr, sr, vertex_nocull(L, sr.d), pend * fr.inv_spp, L.c.pixel, false, cnt))
             break;  // a helper walks it (act: A_CONN)
         L.c.pend = pend;
         L.ray = sr;
@@ -734,6 +774,8 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
 #if !BDPT_SPLIT_CONTINUE
     BDPT_BODY_LIGHT_VERTEX
 #endif
+    }  // PART != 2
+    if (PART == 1) return act;
     BDPT_ACTION(27, act == A_CONN) {  // connectVertices (bdpt.h:434-483) with light vertex ci
         act = A_EYE_CONTINUE;
         if (fr.strategy != 0) break;  // LIGHT/PATH_TRACING builds skip connections (bdpt.h:145)
@@ -779,7 +821,7 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
             const float eyeWeight = eyePathRev_a * (L.c.vcm + eyePrevRev * L.c.vc);
             const float mis = rcp_w(lightWeight + 1.f + eyeWeight);
             const Ray sr = shadow_ray(L.h.p, V.p);
-            if (kTasks && task_push(fr, sr, vertex_nocull(L, sr.d), (Li * mis) * fr.inv_spp, L.c.pixel, false)) {
+            if (kTasks && task_push(L.c, fr, sr, vertex_nocull(L, sr.d), (Li * mis) * fr.inv_spp, L.c.pixel, false, cnt)) {
                 L.c.ci++;  // a helper walks it; the next light vertex now
                 continue;
             }
@@ -808,12 +850,90 @@ __device__ void advance(Lane& L, uint32_t act, const DevScene& sc, const DevFram
         finish<COUNT>(L, fr, fb, cnt);
         act = A_DONE;
     } BDPT_END;
+    return act;
 }
 #undef BDPT_ACTION
 #undef BDPT_END
 #undef BDPT_BODY_LIGHT_VERTEX
 #undef BDPT_BODY_CONTINUE
 #undef BDPT_BODY_LIGHT_NEXT
+
+#if BDPT_HELP && !BDPT_SAMPLER_STATE
+// connectVertices of every owner lane that reached A_CONN in this shading step
+// (bdpt.h:434-483, all its remaining light vertices), flattened over the wave:
+// task i of the prefix sum over the owners' counts runs on lane i mod 64, with the
+// owner's eye vertex from its registers (ds_bpermute), its cold state from LDS and
+// its light vertex from its slot; each connection's shadow ray is pushed to the
+// wave's ring like the serial body's (the same arithmetic in the same order). Called
+// by all 64 lanes between advance<.., 1> and advance<.., 2>; owners leave with
+// ci = nl. When the ring cannot take every connection, nothing is batched and the
+// owners connect one by one in advance<.., 2> (which falls back to tracing them).
+template <bool COUNT>
+__device__ __forceinline__ void conn_batch(Lane& L, bool owner, const DevScene& sc, const DevFrame& fr,
+                                           const LightStore& ls, Counts& cnt) {
+    const int k = owner ? L.c.nl - L.c.ci : 0;
+    const uint64_t om = __ballot(k > 0);
+    if (!om) return;
+    const int me = static_cast<int>(opaque_tid() & 63);
+    int incl = k;  // inclusive prefix sum of k over the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(incl, off);
+        if (me >= off) incl += t;
+    }
+    const int total = __shfl(incl, 63), excl = incl - k;
+    {
+        const TaskCtl ctl = task_ctl(L.c);
+        if (static_cast<uint32_t>(total) > fr.task_cap - (*ctl.tail - *ctl.head)) return;
+    }
+    LaneCold* const wave_cold = &L.c - me;
+    for (int r0 = 0; r0 < total; r0 += 64) {  // (wave-uniform)
+        const int i = r0 + me;
+        int o = -1, j = 0;
+        for (uint64_t m = om; m; m &= m - 1) {  // the owner of task i (scalar loop over the owners)
+            const int b = __ffsll(static_cast<unsigned long long>(m)) - 1;
+            const int eb = __builtin_amdgcn_readlane(excl, b), kb = __builtin_amdgcn_readlane(k, b);
+            if (i >= eb && i < eb + kb) o = b, j = i - eb;
+        }
+        const int src = o >= 0 ? o : me;
+        const f3 hp = mk(__shfl(L.h.p.x, src), __shfl(L.h.p.y, src), __shfl(L.h.p.z, src));
+        const f3 hn = mk(__shfl(L.h.n.x, src), __shfl(L.h.n.y, src), __shfl(L.h.n.z, src));
+        const f3 hwo = mk(__shfl(L.h.wo.x, src), __shfl(L.h.wo.y, src), __shfl(L.h.wo.z, src));
+        const int hmat = __shfl(L.h.mat, src), hshape = __shfl(L.h.shape, src);
+        if (o < 0) continue;
+        const LaneCold& oc = wave_cold[o];
+        const Vertex V = load_vertex_at(ls.at_tid(oc.ci + j, (opaque_tid() & ~63u) + static_cast<uint32_t>(o)));
+        if (COUNT) cnt.c[5]++;
+        f3 dir = hp - V.p;
+        const float invD2 = rcp_w(dot(dir, dir));
+        dir = dir * sqrt_w(invD2);
+        const float cosL = dot(dir, V.n), cosE = dot(-dir, hn);
+        if (cosL <= 0.f || cosE <= 0.f) continue;
+        const BsdfRecord& be = bsdf_of(sc, hmat);
+        const BsdfRecord& bl = bsdf_of(sc, V.mat);
+        const f3 wiL = local_for(bl, V.n, dir);
+        const f3 wiE = local_for(be, hn, -dir);
+        const EvalPdfs eL = bsdf_eval_pdfs(bl, wiL, V.wo), eE = bsdf_eval_pdfs(be, wiE, hwo);
+        f3 Li = eL.f * eE.f;
+        Li = Li * ((V.tp * oc.tp) * invD2);
+        const float eyePathRev_w = eL.fwd;  // (rr = 1: these builds are NO_RR = 1, bdpt.h:461-472)
+        const float lightPrevRev = eL.rev;
+        const float lightPathRev_w = eE.fwd;
+        const float eyePrevRev = eE.rev;
+        const float lightPathRev_a = lightPathRev_w * cosL * invD2;
+        const float eyePathRev_a = eyePathRev_w * cosE * invD2;
+        const float lightWeight = lightPathRev_a * (V.vcm + lightPrevRev * V.vc);
+        const float eyeWeight = eyePathRev_a * (oc.vcm + eyePrevRev * oc.vc);
+        const float mis = rcp_w(lightWeight + 1.f + eyeWeight);
+        const Ray sr = shadow_ray(hp, V.p);
+#if BDPT_GRAZE_IN_DIST
+#error "conn_batch: BDPT_GRAZE_IN_DIST keeps the threshold in Hit::dist"
+#endif
+        task_push(L.c, fr, sr, graze_exempt(sr.d, hn, hshape), (Li * mis) * fr.inv_spp, oc.pixel, false, cnt);
+    }
+    if (k > 0) L.c.ci = L.c.nl;
+}
+#endif
 
 // Pixel and Sampler seed of sample `s` of the shard: seed_base + p * spp + k
 // (the per-(pixel, sample) convention of SURVEY §8c on renderer.cpp:155).

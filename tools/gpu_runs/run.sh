@@ -8,7 +8,8 @@
 #   run.sh tests LABEL [PYTEST_ARGS...]       GPU suite (default: tests -m gpu) + smoke
 #   run.sh ab LABEL REPS "LIB..." [BENCH_ARGS...]
 #                                             A/B bench of variant libraries (lib/libbdpt_amd_<LIB>.so,
-#                                             "default" = the product library), REPS alternating passes,
+#                                             "default" = the product library; LIB:VAR=v,VAR2=w also sets
+#                                             environment for that run), REPS alternating passes,
 #                                             one summary line per run in gpurun_out/LABEL.txt
 #   run.sh abtest LABEL "LIB..." [PYTEST_FILES...]
 #                                             parity suites on variant libraries before an A/B
@@ -33,8 +34,16 @@ import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 c = (d.get("roofline") or {}).get("counts_per_sample") or {}
 p = (d.get("parity") or {}).get("max_rel_l2")
+eff = {}
+if c.get("trav_wave_iters"):
+    eff["trav_simd"] = c["trav_lane_iters"] / c["trav_wave_iters"] / 64
+if c.get("shade_wave_actions"):
+    eff["shade_simd"] = c["shade_lane_actions"] / c["shade_wave_actions"] / 64
 print(sys.argv[1], d["value"], d["ms_per_step"], "parity", p,
-      " ".join(f"{k}={c[k]:.4g}" for k in ("interior_visits", "tri_tests", "loop_clocks", "trav_clocks", "shade_clocks") if k in c))
+      " ".join(f"{k}={c[k]:.4g}" for k in ("interior_visits", "tri_tests", "loop_clocks", "trav_clocks", "shade_clocks",
+                                            "trav_wave_iters", "shade_wave_actions") if k in c),
+      " ".join(f"{k}={v:.3f}" for k, v in eff.items()),
+      "sched", (d.get("roofline") or {}).get("sched_per_sample"))
 PY
 }
 
@@ -63,11 +72,15 @@ ab)
   : > gpurun_out/$LABEL.txt
   for rep in $(seq 1 $REPS); do
     for lib in $LIBS; do
-      out=gpurun_out/${LABEL}_${lib}_$rep.json
-      BDPT_AMD_LIB=$(lib_path $lib) timeout -k 10 300 python3 bench.py --no-cpu --no-parity "$@" > $out 2> ${out%.json}.err
+      # LIB may carry environment settings for the run: name:VAR=v,VAR2=w
+      name=${lib%%:*} envs=""
+      [ "$name" != "$lib" ] && envs=${lib#*:}
+      tag=$(echo "$lib" | tr ':=,' '_-_')
+      out=gpurun_out/${LABEL}_${tag}_$rep.json
+      env ${envs//,/ } BDPT_AMD_LIB=$(lib_path $name) timeout -k 10 300 python3 bench.py --no-cpu --no-parity "$@" > $out 2> ${out%.json}.err
       rc=$?
       if [ $rc -ne 0 ]; then echo "$lib rep $rep rc=$rc" >> gpurun_out/$LABEL.txt; tail -5 ${out%.json}.err; exit $rc; fi
-      summary ${lib}_$rep $out | tee -a gpurun_out/$LABEL.txt
+      summary ${tag}_$rep $out | tee -a gpurun_out/$LABEL.txt
     done
   done
   ;;
