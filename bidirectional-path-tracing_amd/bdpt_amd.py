@@ -213,6 +213,8 @@ def lib():
         L.bdpt_version.restype = ctypes.c_char_p
         L.bdpt_last_kernel.restype = ctypes.c_char_p
         L.bdpt_last_kernel.argtypes = [ctypes.c_void_p]
+        L.bdpt_set_row_order.argtypes = [vp, vp, i32]
+        L.bdpt_get_row_costs.argtypes = [vp, vp, i32]
         L.bdpt_scene_load_obj.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
         L.bdpt_scene_free.argtypes = [vp]
         L.bdpt_scene_get_info.argtypes = [vp, ctypes.POINTER(_SceneInfo)]
@@ -731,9 +733,28 @@ class BDPTIntegrator:
     def synchronize(self) -> None:
         _check(lib().bdpt_synchronize(self._h))
 
+    def set_row_order(self, order) -> None:
+        """Claim order of the shard's local rows for later renders (bdpt_set_row_order);
+        None or [] restores top to bottom. Changes no sample, only which run last."""
+        a = np.ascontiguousarray(np.asarray([] if order is None else order, dtype=np.int32))
+        _check(lib().bdpt_set_row_order(self._h, a.ctypes.data if a.size else None, int(a.size)))
+
+    def row_costs(self, nrows: int) -> np.ndarray:
+        """Queries per local row of the last FLAG_COUNT render (bdpt_get_row_costs)."""
+        out = np.zeros(nrows, np.int64)
+        _check(lib().bdpt_get_row_costs(self._h, out.ctypes.data, int(nrows)))
+        return out
+
     def save(self, path: str) -> None:
         """Integrator::save: self.rgb as the reference's EXR."""
         save_exr(self.rgb, self.config.width, self.config.height, path)
+
+
+def cost_row_order(costs) -> np.ndarray:
+    """Local rows by descending cost (ties top to bottom): the costly rows are claimed
+    first, so the samples still in flight when a shard's work runs out are cheap ones."""
+    c = np.asarray(costs)
+    return np.lexsort((np.arange(c.size), -c)).astype(np.int32)
 
 
 class PathTracerIntegrator(BDPTIntegrator):

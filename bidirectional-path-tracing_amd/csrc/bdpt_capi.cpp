@@ -217,6 +217,10 @@ struct bdpt_ctx {
     uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28, RR)
     uint32_t* park = nullptr;     // Russian roulette: continuation records + parked-slot list (DevFrame::park)
     float4* tasks = nullptr;      // per-wave shadow-ray task rings (DevFrame::tasks; read by BDPT_HELP builds)
+    int32_t* row_order = nullptr;  // bdpt_set_row_order (device copy; DevFrame::row_order)
+    int32_t row_order_n = 0;       // its row count (0: top to bottom)
+    unsigned long long* row_cost = nullptr;  // counting renders: queries per local row (DevFrame::row_cost)
+    int32_t row_cost_cap = 0, row_cost_n = 0;  // its capacity; the rows of the last counting render
     unsigned long long work_init = 0;  // BDPT_SAMPLE_RANGE's first sample (host copy for the async upload)
     uint32_t* capped = nullptr;   // samples that met the Russian-roulette bounds, per call
     unsigned long long* diag = nullptr;  // the BDPT frame kernel's timeline (dev::kDiag*)
@@ -507,7 +511,8 @@ int bdpt_ctx_destroy(bdpt_ctx* c) {
                     static_cast<void*>(c->pt_levels), static_cast<void*>(c->pt_ring), c->pt_dparams,
                     static_cast<void*>(c->mt_ring), static_cast<void*>(c->mt_state), static_cast<void*>(c->capped),
                     static_cast<void*>(c->diag),
-                    static_cast<void*>(c->splat_list), static_cast<void*>(c->park), static_cast<void*>(c->tasks)})
+                    static_cast<void*>(c->splat_list), static_cast<void*>(c->park), static_cast<void*>(c->tasks),
+                    static_cast<void*>(c->row_order), static_cast<void*>(c->row_cost)})
         if (p) (void)hipFree(p);
     if (c->last_use) (void)hipEventDestroy(c->last_use);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -774,6 +779,12 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     dev::DevFrame fr = make_frame(p);
     fr.capped = c->capped;
     fr.tasks = c->tasks;
+    if (c->row_order_n) {
+        if (c->row_order_n != fr.nrows)
+            return fail(BDPT_ERR_INVALID, "the row order set by bdpt_set_row_order has " + std::to_string(c->row_order_n) +
+                                              " rows, the shard " + std::to_string(fr.nrows));
+        fr.row_order = c->row_order;
+    }
     const bool hbm = c->sc.lds_bsdf_off == dev::kNoLds;
     const bool rr = fr.rr_mode != 0;
     const float* eye[1] = {p->camera.eye};
@@ -810,6 +821,19 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
         }
     }
     HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * kCounterWords, st));
+    if ((p->flags & BDPT_FLAG_COUNT) && fr.nrows > 0) {  // queries per local row (bdpt_get_row_costs)
+        if (c->row_cost_cap < fr.nrows) {
+            HIP_TRY(hipStreamSynchronize(st));
+            if (c->row_cost) HIP_TRY(hipFree(c->row_cost));
+            c->row_cost = nullptr;
+            c->row_cost_cap = 0;
+            HIP_TRY(hipMalloc(&c->row_cost, sizeof(unsigned long long) * fr.nrows));
+            c->row_cost_cap = fr.nrows;
+        }
+        HIP_TRY(hipMemsetAsync(c->row_cost, 0, sizeof(unsigned long long) * fr.nrows, st));
+        fr.row_cost = c->row_cost;
+        c->row_cost_n = fr.nrows;
+    }
     HIP_TRY(hipMemsetAsync(c->capped, 0, sizeof(uint32_t), st));
     HIP_TRY(hipMemsetAsync(c->diag, 0, sizeof(unsigned long long) * dev::kDiagWords, st));
     HIP_TRY(hipMemsetAsync(c->diag + dev::kDiagStart, 0xff, sizeof(unsigned long long), st));
@@ -1176,6 +1200,38 @@ int bdpt_debug_math(int32_t device, int32_t fn, const float* x, const float* y, 
 }
 
 const char* bdpt_last_kernel(const bdpt_ctx* c) { return c ? c->last_kernel : ""; }
+
+int bdpt_set_row_order(bdpt_ctx* c, const int32_t* order, int32_t n) {
+    if (!c || n < 0 || (n > 0 && !order)) return fail(BDPT_ERR_INVALID, "bdpt_set_row_order: bad argument");
+    std::vector<char> seen(static_cast<size_t>(n), 0);
+    for (int32_t i = 0; i < n; i++) {
+        if (order[i] < 0 || order[i] >= n || seen[static_cast<size_t>(order[i])])
+            return fail(BDPT_ERR_INVALID, "bdpt_set_row_order: not a permutation of 0..n-1");
+        seen[static_cast<size_t>(order[i])] = 1;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());  // a render in flight may read the previous order
+    if (c->row_order) HIP_TRY(hipFree(c->row_order));
+    c->row_order = nullptr;
+    c->row_order_n = 0;
+    if (n == 0) return BDPT_OK;
+    HIP_TRY(hipMalloc(&c->row_order, sizeof(int32_t) * static_cast<size_t>(n)));
+    HIP_TRY(hipMemcpy(c->row_order, order, sizeof(int32_t) * static_cast<size_t>(n), hipMemcpyHostToDevice));
+    c->row_order_n = n;
+    return BDPT_OK;
+}
+
+int bdpt_get_row_costs(bdpt_ctx* c, int64_t* costs, int32_t n) {
+    if (!c || !costs) return fail(BDPT_ERR_INVALID, "null argument");
+    if (!c->row_cost || n != c->row_cost_n)
+        return fail(BDPT_ERR_INVALID, "bdpt_get_row_costs: no counting render of a " + std::to_string(n) + "-row shard");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(static_cast<size_t>(n));
+    HIP_TRY(hipMemcpy(h.data(), c->row_cost, sizeof(unsigned long long) * static_cast<size_t>(n), hipMemcpyDeviceToHost));
+    for (int32_t i = 0; i < n; i++) costs[i] = static_cast<int64_t>(h[static_cast<size_t>(i)]);
+    return BDPT_OK;
+}
 
 int bdpt_get_stats(bdpt_ctx* c, bdpt_stats* out) {
     if (!c || !out) return fail(BDPT_ERR_INVALID, "null argument");

@@ -189,6 +189,10 @@ struct DevFrame {
     // wave task_cap records of 48 bytes (3 float4), wave w's at tasks + 3 * task_cap * w
     float4* tasks;
     uint32_t task_cap;
+    // the shard's row claim order (bdpt_set_row_order; null: top to bottom) and, in a
+    // counting pass, the queries issued per local row (null otherwise)
+    const int32_t* row_order;
+    unsigned long long* row_cost;
 };
 enum : uint32_t { kParkOn = 1u, kParkResume = 2u };
 enum : uint32_t { kSchedNoCoopGroups = 1u };
@@ -789,11 +793,13 @@ typedef __attribute__((address_space(3))) u32x2 lds_uint2;
 typedef __attribute__((address_space(1))) u32x2 gbl_uint2;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(1))) uint32_t gbl_u32;
+typedef __attribute__((address_space(1))) int32_t gbl_i32;
 #else
 typedef u32x2 lds_uint2;
 typedef u32x2 gbl_uint2;
 typedef uint32_t lds_u32;
 typedef uint32_t gbl_u32;
+typedef int32_t gbl_i32;
 #endif
 // threadIdx.x, re-read at each use (opaque to the optimiser): per-lane
 // addresses derived from it at their use are not held in registers across the

@@ -428,6 +428,9 @@ __device__ __forceinline__ void finish(Lane& L, const DevFrame& fr, float* __res
         cnt.c[7] += L.rng.n;
         cnt.m[1] = max(cnt.m[1], static_cast<uint32_t>(L.c.depth));
         cnt.m[2] = max(cnt.m[2], static_cast<uint32_t>(L.c.steps));
+        if (fr.row_cost)  // the sample's queries to its local row (bdpt_get_row_costs)
+            gadd(fr.row_cost + (L.c.pixel / fr.W - fr.row_offset) / fr.row_stride,
+                 static_cast<unsigned long long>(L.c.steps));
     }
     // rgb[p] += acc * (1 / spp) (renderer.cpp:202), one sample at a time.
     if (!(fr.flags & kFlagNoEyeAccum) && (L.c.Li.x != 0.f || L.c.Li.y != 0.f || L.c.Li.z != 0.f)) {
@@ -939,7 +942,9 @@ __device__ __forceinline__ void conn_batch(Lane& L, bool owner, const DevScene& 
 // (the per-(pixel, sample) convention of SURVEY §8c on renderer.cpp:155).
 __device__ __forceinline__ uint32_t sample_seed(uint64_t s, const DevFrame& fr, int& pixel) {
     const uint64_t per_row = static_cast<uint64_t>(fr.W) * fr.spp;
-    const uint64_t lr = s / per_row, q = s % per_row;
+    uint64_t lr = s / per_row;
+    const uint64_t q = s % per_row;
+    if (fr.row_order) lr = static_cast<uint64_t>(((const gbl_i32*)fr.row_order)[lr]);  // bdpt_set_row_order
     const int j = static_cast<int>(q / fr.spp), k = static_cast<int>(q % fr.spp);
     const int row = fr.row_offset + static_cast<int>(lr) * fr.row_stride;
     pixel = row * fr.W + j;

@@ -153,7 +153,9 @@ typedef struct {
     int64_t sched[4];        /* counting pass (BDPT_FLAG_COUNT), the connection tasks a wave holds when it
                                 shades (connectVertices still to run, connectToLight + the connections of a
                                 new eye vertex, connectToCamera of a new light vertex): summed over the
-                                shading steps, the shading steps, steps with >= 32 and with >= 64 tasks */
+                                shading steps, the shading steps, steps with >= 32 and with >= 64 tasks.
+                                Builds whose waiting lanes walk the shadow rays (BDPT_HELP): tasks pushed,
+                                pushes refused (ring full), claim rounds, tasks claimed */
     int64_t parked_samples;  /* Russian roulette: walks handed to the continuation pass's chain kernel
                                 (deeper than BDPT_PARK_DEPTH bounces; a sample may be handed over again) */
     int64_t rr_long_walks_max;  /* Russian roulette: the most subpaths deeper than 512 bounces one wave held
@@ -293,6 +295,20 @@ int bdpt_get_stats(bdpt_ctx* ctx, bdpt_stats* out);
 const char* bdpt_last_kernel(const bdpt_ctx* ctx);
 /* Waits for all work queued by this context (on every stream it was given). */
 int bdpt_synchronize(bdpt_ctx* ctx);
+/* (new) Claim order of the shard's rows for the context's later bdpt_render calls: order[i]
+ * is the i-th row claimed (a permutation of the shard's local rows 0..n-1, local row r =
+ * image row row_offset + r * row_stride); n = 0 restores top-to-bottom. The reference's
+ * offline loop hands rows to its threads in order (parallel_for over rows,
+ * renderer.cpp:157, parallelfor.h:25-65); the order changes no sample (each keeps its
+ * (pixel, sample) seed) and so no result beyond the float addition order, only which
+ * samples run last: a render whose shard has a different row count fails
+ * (BDPT_ERR_INVALID). Costly rows first leaves cheap samples in flight when the work runs
+ * out, which shortens the persistent grid's end tail (each of N ranks pays it once). */
+int bdpt_set_row_order(bdpt_ctx* ctx, const int32_t* order, int32_t n);
+/* (new) Per local row of the last BDPT_FLAG_COUNT render's shard, the ray queries its
+ * samples issued (a cost estimate for bdpt_set_row_order). Returns BDPT_ERR_INVALID when
+ * n differs from that shard's row count. Synchronous. */
+int bdpt_get_row_costs(bdpt_ctx* ctx, int64_t* costs, int32_t n);
 
 /* ---- the reference's path tracer on the same substrate (src/integrators/path.h) ---- */
 typedef struct {

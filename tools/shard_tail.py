@@ -3,6 +3,10 @@ one GPU: the strong-scaling tail a persistent grid pays when each of N ranks
 renders 1/N of the frame (lanes idle once the shard's work counter runs out).
 
     python tools/shard_tail.py [scene W H spp] [N...]
+
+Each shard is measured twice: rows claimed top to bottom, and costly rows first
+(bdpt_set_row_order with the queries per row of a 4-spp counting pass of the
+same shard, bdpt_amd.cost_row_order).
 """
 import os
 import sys
@@ -26,22 +30,32 @@ def main():
     integ = bdpt_amd.BDPTIntegrator(bdpt_amd.Scene(variants.obj_path(scene)), cfg, device=0)
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
-    full = None
+    ccfg = bdpt_amd.Config(camera=cfg.camera, width=W, height=H, spp=min(spp, 4), rr_depth=cfg.rr_depth)
+    counter = bdpt_amd.BDPTIntegrator(integ.scene, ccfg, device=0)
+    cfb = torch.zeros_like(fb)
+    full = {}
     for n in ns:
-        ms, tails = [], []
-        for rep in range(3):
-            fb.zero_()
-            integ.render_device(fb.data_ptr(), stream, row_offset=0, row_stride=n)
-            st = integ.stats()
-            ms.append(st["kernel_ms"])
-            tails.append(st.get("tail_ms", 0.0))
-        t = min(ms[1:])
-        tail = min(tails[1:])
-        if n == 1:
-            full = t
-        ideal = full / n if full else float("nan")
-        print(f"row_stride {n}: kernel {t:.2f} ms, full/{n} = {ideal:.2f} ms, efficiency {ideal / t:.3f}, "
-              f"end tail {tail:.2f} ms", flush=True)
+        nrows = len(range(0, H, n))
+        counter.render_device(cfb.data_ptr(), stream, row_offset=0, row_stride=n, flags=bdpt_amd.FLAG_COUNT)
+        order = bdpt_amd.cost_row_order(counter.row_costs(nrows))
+        for kind in ("top-down", "cost"):
+            integ.set_row_order(order if kind == "cost" else None)
+            ms, tails = [], []
+            for rep in range(3):
+                fb.zero_()
+                integ.render_device(fb.data_ptr(), stream, row_offset=0, row_stride=n)
+                st = integ.stats()
+                ms.append(st["kernel_ms"])
+                tails.append(st.get("tail_ms", 0.0))
+            t = min(ms[1:])
+            tail = min(tails[1:])
+            if n == 1:
+                full[kind] = t
+            f = full.get(kind)
+            ideal = f / n if f else float("nan")
+            print(f"row_stride {n} ({kind} rows): kernel {t:.2f} ms, full/{n} = {ideal:.2f} ms, "
+                  f"efficiency {ideal / t:.3f}, end tail {tail:.2f} ms", flush=True)
+        integ.set_row_order(None)
 
 
 if __name__ == "__main__":
