@@ -217,6 +217,7 @@ struct bdpt_ctx {
     uint32_t* mt_ring = nullptr;  // BDPT megakernel: MT19937 continuation past 227 draws (rrDepth > 28, RR)
     uint32_t* park = nullptr;     // Russian roulette: continuation records + parked-slot list (DevFrame::park)
     float4* tasks = nullptr;      // per-wave shadow-ray task rings (DevFrame::tasks; read by BDPT_HELP builds)
+    uint32_t task_cap = 0;        // their capacity (tasks per wave, a power of two)
     int32_t* row_order = nullptr;  // bdpt_set_row_order (device copy; DevFrame::row_order)
     int32_t row_order_n = 0;       // its row count (0: top to bottom)
     unsigned long long* row_cost = nullptr;  // counting renders: queries per local row (DevFrame::row_cost)
@@ -669,7 +670,12 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     HIP_TRY(hipMalloc(&c->gstack, sizeof(uint2) * std::max<size_t>(1, spill_mega)));
     // shadow-ray task rings, one per wave of the persistent grid (4096 waves x 256 x 48 B = 50 MB on
     // 256 CUs); only builds with BDPT_HELP read them
-    HIP_TRY(hipMalloc(&c->tasks, sizeof(float4) * 3 * kTaskCap * (c->nslots / 64)));
+    c->task_cap = kTaskCap;
+    if (const char* e = std::getenv("BDPT_TASK_CAP")) {  // (sweeps) a power of two in [64, 4096]
+        const int v = std::atoi(e);
+        if (v >= 64 && v <= 4096 && (v & (v - 1)) == 0) c->task_cap = static_cast<uint32_t>(v);
+    }
+    HIP_TRY(hipMalloc(&c->tasks, sizeof(float4) * 3 * c->task_cap * (c->nslots / 64)));
     *out = c.release();
     return BDPT_OK;
 }
@@ -712,7 +718,6 @@ static dev::DevFrame make_frame(const bdpt_frame_params* p) {
     // BDPT_COOP_GROUPS=0 override the build's depth and grouped walks (tests reach the
     // grouped and turn-taking walks on small frames this way; the results are the same)
     fr.express_depth = kExpressDepth;
-    fr.task_cap = kTaskCap;
     if (const char* e = std::getenv("BDPT_EXPRESS_DEPTH")) fr.express_depth = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("BDPT_COOP_GROUPS")) fr.sched_flags |= *e == '0' ? dev::kSchedNoCoopGroups : 0u;
     return fr;
@@ -779,6 +784,7 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     dev::DevFrame fr = make_frame(p);
     fr.capped = c->capped;
     fr.tasks = c->tasks;
+    fr.task_cap = c->task_cap;
     if (c->row_order_n) {
         if (c->row_order_n != fr.nrows)
             return fail(BDPT_ERR_INVALID, "the row order set by bdpt_set_row_order has " + std::to_string(c->row_order_n) +
