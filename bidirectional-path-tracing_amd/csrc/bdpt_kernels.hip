@@ -40,7 +40,12 @@
 #endif
 
 // Shadow-ray tasks walked by waiting lanes (bdpt_path.hpp task_push): only the
-// overlapped frame kernels without Russian roulette build them.
+// overlapped frame kernels without Russian roulette build them (round 6: Caustic
+// 512^2 x 256 288.5 -> 323.4 Msamples/s, synth1m 1024^2 x 64 203.2 -> 218.9,
+// HardLight 512^2 x 256 1478.5 -> 1485.1).
+#ifndef BDPT_HELP
+#define BDPT_HELP 1
+#endif
 #if (defined(BDPT_RR) && BDPT_RR) || (defined(BDPT_SAMPLER_STATE) && BDPT_SAMPLER_STATE) || \
     (defined(BDPT_OVERLAP) && !BDPT_OVERLAP)
 #undef BDPT_HELP
@@ -289,14 +294,14 @@ struct KParams {
 #define BDPT_COOP_GROUPS 1  // express waves with 2-4 long walks walk them at once in groups of 32 / 16 lanes (coop_closest_groups; RR Caustic frames 42.7-45.2 s vs 43.8-54.0)
 #endif
 #ifndef BDPT_HELP_BATCH
-#define BDPT_HELP_BATCH 0  // BDPT_HELP: the shading step's connections flattened over the wave (conn_batch)
+#define BDPT_HELP_BATCH 1  // BDPT_HELP: the shading step's connections flattened over the wave (conn_batch; serial: 283.0 vs 322.8)
 #endif
 #if !BDPT_HELP
 #undef BDPT_HELP_BATCH
 #define BDPT_HELP_BATCH 0
 #endif
 #ifndef BDPT_HELP_MIN
-#define BDPT_HELP_MIN 1  // BDPT_HELP: fewest waiting lanes that start a claim round (unless the ring holds fewer tasks)
+#define BDPT_HELP_MIN 16  // BDPT_HELP: fewest waiting lanes that start a claim round (unless the ring holds fewer tasks; 1 / 8 / 12 / 16 / 20 / 24: 264.9 / 322.7 / 323.3 / 323.4 / 319.8 / 266.4)
 #endif
 #ifndef BDPT_TAIL_PROBE
 #define BDPT_TAIL_PROBE 0  // measurement only (non-RR builds): the drain phase in the RR diag words (tools/tail_probe.py)
