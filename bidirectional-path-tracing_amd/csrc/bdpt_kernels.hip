@@ -300,6 +300,12 @@ struct KParams {
 #undef BDPT_HELP_BATCH
 #define BDPT_HELP_BATCH 0
 #endif
+#ifndef BDPT_HELP_SREG
+#define BDPT_HELP_SREG 0  // BDPT_HELP: the ring positions held in SGPRs during the walk loop (no LDS reads per iteration)
+#endif
+#ifndef BDPT_HELP_DEFER
+#define BDPT_HELP_DEFER 0  // BDPT_HELP: a claimed task's walk begins one walk iteration after its record loads
+#endif
 #ifndef BDPT_HELP_MIN
 #define BDPT_HELP_MIN 16  // BDPT_HELP: fewest waiting lanes that start a claim round (unless the ring holds fewer tasks; 1 / 8 / 12 / 16 / 20 / 24: 264.9 / 322.7 / 323.3 / 323.4 / 319.8 / 266.4)
 #endif
@@ -398,8 +404,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     // shading step (the frame cannot end before it does).
     bool long_walk = false;
 #if BDPT_HELP
-    // helping: the lane walks a task's shadow ray (tracing is set too; its ring slot in rt)
+    // helping: the lane walks a task's shadow ray (tracing is set too) or, with BDPT_HELP_DEFER,
+    // waits one iteration for its claimed record (hwait)
     bool helping = false;
+#if BDPT_HELP_DEFER
+    bool hwait = false;
+#endif
     {
         const TaskCtl ctl = task_ctl(L.c);
         if (lane0()) *ctl.head = *ctl.tail = 0u;
@@ -718,10 +728,16 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // on the lane's LDS stack traffic every iteration
         const int steady_ready = P->fr.shade_ready > 0 ? P->fr.shade_ready : BDPT_SHADE_READY;
 #endif
+#if BDPT_HELP && BDPT_HELP_SREG
+        // the ring's positions in scalar registers while the wave walks (pushes happen
+        // only in the shading step; claims below write the head back)
+        uint32_t qhead = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(*task_ctl(L.c).head)));
+        const uint32_t qtail = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(*task_ctl(L.c).tail)));
+#endif
         for (;;) {  // walk until enough lanes have a result to shade
 #if BDPT_HELP
             uint64_t tr = __ballot(tracing);
-            const uint64_t ready = __ballot(has_res && !tracing);  // helpers shade after their walk
+            const uint64_t ready = __ballot(has_res && !helping);  // helpers shade after their walk
             if (popc64(ready) >= (BDPT_TAIL_SHADE == 1 && exhausted ? 1
                                   : BDPT_TAIL_SHADE == 2 && exhausted ? max(1, (popc64(tr | ready) * BDPT_TAIL_FRAC) >> 3)
                                                                       : steady_ready))
@@ -729,12 +745,48 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             // Lanes that wait (a result kept, or no sample) claim the ring's oldest
             // tasks, one each, and walk their shadow rays with the walk code below.
             bool hfin = false;  // a helper walk that ended in this iteration (result in ts.best)
+            // a claimed task's walk begins: the root's LDS tests, or at once a result
+            auto help_begin = [&](float near) {
+                q_any = true;
+                if (COUNT) cnt.c[1]++;
+                ri = ray_inv(L.ray, near);
+                ts.best = -1;
+                if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root: unoccluded
+                    hfin = true;
+                } else if (!ri.fast || far_origin(P->sc, L.ray.o)) {  // the reference's tree, unculled
+                    const TravResult qr = traverse_binary<COUNT, Stack>(P->sc, L.ray, true, false, stk);
+                    if (COUNT) cnt.c[2] += qr.nodes, cnt.c[3] += qr.tris, cnt.c[15] += qr.exact;
+                    ts.best = qr.best;
+                    hfin = true;
+                } else {
+                    ts = trav_begin(tsc, L.ray);
+                    tracing = true;
+#if BDPT_ROOT_LDS
+                    if (root_in_lds && !walk_begin_lds<COUNT, SLACK>(root_lds, L.ray, ri, true, ts, stk, cnt)) {
+                        tracing = false;  // no child hit: unoccluded
+                        hfin = true;
+                    }
+#endif
+                }
+            };
+#if BDPT_HELP_DEFER
+            if (hwait) {  // claimed in the previous iteration: its record has arrived meanwhile
+                hwait = false;
+                L.c.pend = mk(ts.best_t, ts.best_u, ts.best_v);
+                L.c.pend_px = static_cast<int>(ts.link);
+                help_begin(ri.near);
+            }
+#endif
             {
                 const TaskCtl ctl = task_ctl(L.c);
+#if BDPT_HELP_SREG
+                const uint32_t head = qhead, tail = qtail;
+#else
                 const uint32_t head = *ctl.head, tail = *ctl.tail;
+#endif
                 // (a lane waiting on its own shadow ray, pushed by itself when the ring was
                 // full, keeps its pending contribution in L.c.pend: it does not help)
-                const bool cand = !tracing && (has_res ? !is_shadow_state(L.state) : L.state == ST_IDLE);
+                const bool cand = !helping && !tracing && (has_res ? !is_shadow_state(L.state) : L.state == ST_IDLE);
                 uint64_t cm = head != tail ? __ballot(cand) : 0ull;
                 // claim rounds only with enough takers (each round exposes one record load):
                 // BDPT_HELP_MIN lanes, or any once the wave's own walks have ended
@@ -744,6 +796,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     const uint32_t n = min(static_cast<uint32_t>(popc64(cm)), tail - head);
                     const uint32_t rank = static_cast<uint32_t>(lanes_below(cm));
                     *ctl.head = head + n;
+#if BDPT_HELP_SREG
+                    qhead = head + n;
+#endif
                     if (cand && rank < n) {
                         if (has_res) help_compact(L, res, rt, ru, rv, P->sc);  // frees L.ray
                         const uint32_t slot = (head + rank) & (P->fr.task_cap - 1);
@@ -753,37 +808,30 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                                      c = gld4(task_vec(ring, cap, slot, 2));
                         if (COUNT) cnt.q[3]++;  // (counting pass: claims)
                         L.ray = Ray{xyz(a), xyz(b), kEpsilon, a.w};
+                        helping = true;
+#if BDPT_HELP_DEFER
+                        // the walk begins next iteration (the loads land meanwhile): the near
+                        // cull, contribution and pixel wait in the lane's idle walk registers
+                        ri.near = b.w;
+                        ts.best_t = c.x, ts.best_u = c.y, ts.best_v = c.z;
+                        ts.link = __float_as_uint(c.w);
+                        hwait = true;
+#else
                         // the contribution and pixel into the lane's (free) pending-connection
                         // fields: the slot may be pushed over once claimed
                         L.c.pend = xyz(c);
                         L.c.pend_px = __float_as_int(c.w);
-                        q_any = true;
-                        helping = true;
-                        if (COUNT) cnt.c[1]++;
-                        ri = ray_inv(L.ray, b.w);
-                        ts.best = -1;
-                        if (L.ray.min_t > L.ray.max_t) {  // the reference culls the root: unoccluded
-                            hfin = true;
-                        } else if (!ri.fast || far_origin(P->sc, L.ray.o)) {  // the reference's tree, unculled
-                            const TravResult qr = traverse_binary<COUNT, Stack>(P->sc, L.ray, true, false, stk);
-                            if (COUNT) cnt.c[2] += qr.nodes, cnt.c[3] += qr.tris, cnt.c[15] += qr.exact;
-                            ts.best = qr.best;
-                            hfin = true;
-                        } else {
-                            ts = trav_begin(tsc, L.ray);
-                            tracing = true;
-#if BDPT_ROOT_LDS
-                            if (root_in_lds && !walk_begin_lds<COUNT, SLACK>(root_lds, L.ray, ri, true, ts, stk, cnt)) {
-                                tracing = false;  // no child hit: unoccluded
-                                hfin = true;
-                            }
+                        help_begin(b.w);
 #endif
-                        }
                     }
                 }
             }
             tr = __ballot(tracing);
+#if BDPT_HELP_DEFER
+            if (!tr && !__ballot(hfin) && !__ballot(hwait)) break;
+#else
             if (!tr && !__ballot(hfin)) break;
+#endif
 #else
             const uint64_t tr = __ballot(tracing);
             if (!tr) break;
@@ -846,7 +894,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
         }
         const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
-        const bool shade_now = has_res && !(BDPT_HELP && tracing);  // (a helper mid-walk shades next time)
+        const bool shade_now = has_res && !(BDPT_HELP && helping);  // (a helper mid-walk shades next time)
 #if BDPT_HELP_BATCH
         uint32_t act2 = A_DONE;
 #endif
