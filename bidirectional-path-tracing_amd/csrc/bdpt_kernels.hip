@@ -301,10 +301,10 @@ struct KParams {
 #define BDPT_HELP_BATCH 0
 #endif
 #ifndef BDPT_HELP_SREG
-#define BDPT_HELP_SREG 0  // BDPT_HELP: the ring positions held in SGPRs during the walk loop (no LDS reads per iteration)
+#define BDPT_HELP_SREG 1  // BDPT_HELP: the ring positions held in SGPRs during the walk loop (no LDS reads per iteration; 324.6 vs 322.7)
 #endif
 #ifndef BDPT_HELP_DEFER
-#define BDPT_HELP_DEFER 0  // BDPT_HELP: a claimed task's walk begins one walk iteration after its record loads
+#define BDPT_HELP_DEFER 0  // BDPT_HELP: a claimed task's walk begins one walk iteration after its record loads (305.8 vs 323.5: not kept)
 #endif
 #ifndef BDPT_HELP_MIN
 #define BDPT_HELP_MIN 16  // BDPT_HELP: fewest waiting lanes that start a claim round (unless the ring holds fewer tasks; 1 / 8 / 12 / 16 / 20 / 24: 264.9 / 322.7 / 323.3 / 323.4 / 319.8 / 266.4)
