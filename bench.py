@@ -250,6 +250,11 @@ def main() -> None:
                          "1 emitter + 1 BSDF sample) on the same substrate, for comparison")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the in-run parity check of the GPU row shard against the CPU reference frame")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="BDPT frames in flight: 1 = each step waits for its frame; 2 = consecutive steps' frames "
+                         "overlap (two contexts, streams and framebuffers): the next frame's blocks start on the "
+                         "CUs the previous frame's draining waves leave, hiding the persistent grid's end tail "
+                         "(every frame is still rendered whole and reduced; the clock brackets all K steps)")
     ap.add_argument("--profiles", default=os.path.join(REPO, "profiles"),
                     help="directory of kernel-build-stamped PMC summaries (pmc_<workload>.json, "
                          "pmc_deep_<workload>.json) for roofline.traffic / limiter")
@@ -318,8 +323,54 @@ def main() -> None:
             torch.cuda.synchronize(dev)
             reduce_ms.append((time.perf_counter() - r0) * 1e3)
 
+    # Pipelined frames (--pipeline 2): step i renders on context / stream / framebuffer i mod 2;
+    # a context's stats are read (which waits for its frame) only when it is reused two steps
+    # later, so the other stream's frame is already queued behind it.
+    nctx = max(1, args.pipeline) if args.integrator == "bdpt" else 1
+    if nctx > 1:
+        integs = [integ] + [bdpt_amd.BDPTIntegrator(integ.scene, cfg, device=gpu if world > 1 else 0)
+                            for _ in range(nctx - 1)]
+        fbs = [fb] + [torch.zeros_like(fb) for _ in range(nctx - 1)]
+        tstreams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nctx - 1)]
+        pending = [False] * nctx
+        nstep = [0]
+
+        def collect(j):
+            st = integs[j].stats()  # waits for context j's frame
+            kernel_ms.append(st["kernel_ms"])
+            tail_ms.append(st.get("tail_ms", 0.0))
+            capped.append(st.get("capped_samples", 0))
+            parked.append(st.get("parked_samples", 0))
+            longs.append(st.get("rr_long_walks_max", 0))
+            express.append(st.get("rr_express_iters", [0, 0, 0]))
+            if st.get("schedule_errors"):
+                raise RuntimeError(f"{st['schedule_errors']} schedule errors in the render")
+            pending[j] = False
+
+        def step():  # noqa: F811 (the pipelined step)
+            j = nstep[0] % nctx
+            nstep[0] += 1
+            if pending[j]:
+                collect(j)
+            with torch.cuda.stream(tstreams[j]):
+                fbs[j].zero_()
+                integs[j].render_device(fbs[j].data_ptr(), tstreams[j].cuda_stream, row_offset=row_offset,
+                                        row_stride=row_stride)
+                if world > 1:  # the exchange step, on the frame's own stream
+                    bdpt_dist.reduce_framebuffer(fbs[j], dst=0)
+            pending[j] = True
+
+        def drain():
+            for j in range(nctx):
+                if pending[j]:
+                    collect(j)
+    else:
+        def drain():
+            pass
+
     for _ in range(args.warmup):
         step()
+    drain()
     kernel_ms.clear()
     reduce_ms.clear()
     tail_ms.clear()
@@ -333,6 +384,7 @@ def main() -> None:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -460,6 +512,7 @@ def main() -> None:
                      else "synthetic camera samples over a generated 1M-triangle scene"),
             "config": {"workload": workload, "scene": SCENE_LABEL.get(args.scene, args.scene),
                        "width": W, "height": H, "spp": spp, "rr_depth": rr, "samples_per_step": samples_total,
+                       "frames_in_flight": nctx,
                        "parallelism": (f"{world}-way row-interleaved shards + one framebuffer sum-reduce "
                                        f"({ranks['backend']})" if ranks else "one GPU, whole image (no reduce)")},
             "roofline": roof,

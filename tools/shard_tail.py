@@ -56,6 +56,32 @@ def main():
             print(f"row_stride {n} ({kind} rows): kernel {t:.2f} ms, full/{n} = {ideal:.2f} ms, "
                   f"efficiency {ideal / t:.3f}, end tail {tail:.2f} ms", flush=True)
         integ.set_row_order(None)
+    # Throughput form: K frames of the shard back to back with two frames in flight (two
+    # contexts and streams, bench.py --pipeline 2), wall time per frame against the full
+    # frame's the same way.
+    ctxs = [integ, bdpt_amd.BDPTIntegrator(integ.scene, cfg, device=0)]
+    fbs = [fb, torch.zeros_like(fb)]
+    ss = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    import time
+    pfull = None
+    for n in ns:
+        def run(k):
+            for i in range(k):
+                j = i % 2
+                with torch.cuda.stream(ss[j]):
+                    fbs[j].zero_()
+                    ctxs[j].render_device(fbs[j].data_ptr(), ss[j].cuda_stream, row_offset=0, row_stride=n)
+            torch.cuda.synchronize()
+        K = 4 * n
+        run(2)
+        t0 = time.perf_counter()
+        run(K)
+        per = (time.perf_counter() - t0) / K * 1e3
+        if n == 1:
+            pfull = per
+        ideal = pfull / n if pfull else float("nan")
+        print(f"row_stride {n} (2 frames in flight, {K} frames): {per:.2f} ms per frame, full/{n} = {ideal:.2f} ms, "
+              f"efficiency {ideal / per:.3f}", flush=True)
 
 
 if __name__ == "__main__":
