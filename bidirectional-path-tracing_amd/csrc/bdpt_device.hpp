@@ -18,6 +18,10 @@ constexpr float kInvTwoPi = 0.15915494309189533577f;  // platform.h:52
 constexpr float kEpsilon = 1e-8f;                     // platform.h:56
 constexpr float kTriMinT = 0x1.0624dep-10f;           // smallest float t with (double)t > 1e-3 (accel.h:43)
 constexpr int kCounters = 32;
+#ifndef BDPT_HELP_CLOCKS
+#define BDPT_HELP_CLOCKS 0  // (bdpt_kernels.hip) the stack-depth probe words carry other clocks
+#endif
+
 #ifndef BDPT_TRAV_WHILE_WHILE
 #define BDPT_TRAV_WHILE_WHILE 1  // megakernel traversal loop shape (0: one node or leaf per iteration)
 #endif
@@ -1282,7 +1286,7 @@ __device__ __forceinline__ bool trav_node_vals(const WNode& n, const Ray& r, con
     if (lnk[3] != kEmptyLinkDev) stk.put(ts.sp++, lnk[3], key[3]);
     if (lnk[2] != kEmptyLinkDev) stk.put(ts.sp++, lnk[2], key[2]);
     if (lnk[1] != kEmptyLinkDev) stk.put(ts.sp++, lnk[1], key[1]);
-    if (COUNT) {  // stack-depth probe: entries held at depth >= 8, >= 12, >= 16
+    if (COUNT && !BDPT_HELP_CLOCKS) {  // stack-depth probe: entries held at depth >= 8, >= 12, >= 16
         cnt.c[16] += ts.sp > 8 ? ts.sp - 8 : 0;
         cnt.c[17] += ts.sp > 12 ? ts.sp - 12 : 0;
         cnt.c[18] += ts.sp > 16 ? ts.sp - 16 : 0;
@@ -1301,7 +1305,20 @@ struct RootLds {
     WNode root;
     WNode kid[4];
 };
+#ifndef BDPT_COOP_ROOT_LDS
+#define BDPT_COOP_ROOT_LDS 0  // cooperative walks read the root and its children from the block's LDS copy
+#endif
 __device__ __forceinline__ bool root_lds_usable(const DevScene& sc) { return !(sc.wroot_link & kLeafBit); }
+__device__ __forceinline__ WNode coop_node(const TravScene& sc, uint32_t link, const RootLds* rl) {
+    if (BDPT_COOP_ROOT_LDS && rl) {
+        if (link == sc.wroot_link) return rl->root;
+        const float4 lk = rl->root.v[kNodeLinks];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (link == __float_as_uint((&lk.x)[k])) return rl->kid[k];  // (a leaf link never reaches here)
+    }
+    return load_wnode(sc.wnodes, link);
+}
 __device__ __forceinline__ void root_lds_fill(RootLds& m, const DevScene& sc) {
     if (!root_lds_usable(sc)) return;
     const float4* const base = BDPT_QNODES ? sc.qnodes : sc.wnodes;
@@ -1497,12 +1514,18 @@ struct CoopStack {
         return (coop_lds_e*)base + (stride ? (e >> 6) * stride + (e & 63) : e);
     }
 };
+// A node of a cooperative walk: from the block's LDS copy when it is the root or
+// one of its interior children (RootLds; rl non-null), else from HBM. The
+// trapped glass chains' walks start at the root, so their first two rounds read
+// LDS instead of waiting on two dependent loads (BDPT_COOP_ROOT_LDS).
+struct RootLds;
+__device__ __forceinline__ WNode coop_node(const TravScene& sc, uint32_t link, const RootLds* rl);
 // BATCH: coop_leaf (a leaf's triangle loads issued together, 48 more live
 // registers) rather than wleaf_tests.
 template <bool SLACK, bool BATCH = true>
 __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, const RayInv& ri, float bound,
                                              CoopStack stk, int cap, float& best_t, int& best, float& best_u,
-                                             float& best_v, uint32_t* rounds = nullptr) {
+                                             float& best_v, uint32_t* rounds = nullptr, const RootLds* rl = nullptr) {
     const uint32_t lane = __lane_id();
     best_t = bound < r.max_t ? bound : r.max_t, best = -1, best_u = best_v = 0.f;
     if (lane == 0) *stk.at(0) = u32x2{sc.wroot_link, __float_as_uint(-__builtin_inff())};
@@ -1529,7 +1552,7 @@ __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, 
                     wleaf_tests<false>(sc.wtri, sc.lbox, e.x, r, ri, false, lt, lb, lu, lv, cnt);
                 }
             }
-            else node_child_keys<SLACK>(load_wnode(sc.wnodes, e.x), r, ri, far, key, lnk);
+            else node_child_keys<SLACK>(coop_node(sc, e.x, rl), r, ri, far, key, lnk);
         }
         // the wave's lexicographic minimum of (t, index) over the lanes that found
         // a better hit (usually none or one): a scalar loop over their keys
@@ -1573,7 +1596,8 @@ __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, 
 template <bool SLACK>
 __device__ __forceinline__ bool coop_closest_groups(const TravScene& sc, const Ray& r, const RayInv& ri, float bound,
                                                     bool active, CoopStack stk, int base, int cap, int G,
-                                                    float& best_t, int& best, float& best_u, float& best_v) {
+                                                    float& best_t, int& best, float& best_u, float& best_v,
+                                                    const RootLds* rl = nullptr) {
     const uint32_t lane = __lane_id();
     const int gl = static_cast<int>(lane) & (G - 1);
     const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (static_cast<int>(lane) - gl);
@@ -1597,7 +1621,7 @@ __device__ __forceinline__ bool coop_closest_groups(const TravScene& sc, const R
                 Counts cnt;  // (not a counting pass)
                 wleaf_tests<false>(sc.wtri, sc.lbox, e.x, r, ri, false, lt, lb, lu, lv, cnt);
             } else {
-                node_child_keys<SLACK>(load_wnode(sc.wnodes, e.x), r, ri, far, key, lnk);
+                node_child_keys<SLACK>(coop_node(sc, e.x, rl), r, ri, far, key, lnk);
             }
         }
         // each group's lexicographic minimum of (t, index) over its improving lanes

@@ -246,6 +246,81 @@ __device__ __forceinline__ bool park_lane(const DevFrame& fr, uint32_t nslots, u
 #define BDPT_BUSY(st) ((st) != ST_IDLE)
 #endif
 
+#if BDPT_RR == 1 && !BDPT_SAMPLER_STATE && BDPT_EXPRESS_CHAIN == 2
+// The lone long walk's chain of delta bounces (express mode, one busy lane b): each
+// closest hit walked by the whole wave (coop_closest), the bounce itself on lane b,
+// back to back until the chain reaches a vertex the sweep must shade. Out of line,
+// called by all 64 lanes, so the megakernel's register allocation is not sized for
+// it. Returns -1 with the last walk's result in (t, r, u, v, ok) for the sweep; 0 when
+// the chain ended here (lane b: ST_DEFER or finished); 2 when lane b's next query
+// must begin at the loop top (the reference's tree, or a culled root).
+template <bool SLACK>
+__device__ __noinline__ int express_chain(Lane& Lcaller, int b, RayInv& ri_caller, const DevScene& sc,
+                                          const DevFrame& fr, float* __restrict__ fb, const TravScene& tsc,
+                                          uint2* stack_base, const RootLds* coop_rl, float& t, int& r, float& u,
+                                          float& v, bool& ok) {
+    Counts cnt;  // (not a counting pass)
+    Lane L(Lcaller.c);
+    L.rng = Lcaller.rng, L.state = Lcaller.state, L.ray = Lcaller.ray, L.h = Lcaller.h;
+    RayInv ri = ri_caller;
+    const int me = static_cast<int>(__lane_id());
+    const CoopStack cs{stack_base, kBlock};
+    int bounced = -1;
+    for (;;) {
+        Ray q;
+        q.o = mk(__shfl(L.ray.o.x, b), __shfl(L.ray.o.y, b), __shfl(L.ray.o.z, b));
+        q.d = mk(__shfl(L.ray.d.x, b), __shfl(L.ray.d.y, b), __shfl(L.ray.d.z, b));
+        q.min_t = __shfl(L.ray.min_t, b), q.max_t = __shfl(L.ray.max_t, b);
+        RayInv qi;
+        qi.inv = mk(__shfl(ri.inv.x, b), __shfl(ri.inv.y, b), __shfl(ri.inv.z, b));
+        qi.near = __shfl(ri.near, b);
+        qi.fast = true;
+        const float guess = BDPT_GRAZE_IN_DIST ? -1.f : __shfl(L.h.dist, b);
+        r = -1;
+        ok = true;
+        for (int pass = guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
+            const float bound = pass == 0 ? 2.f * guess : q.max_t;
+            ok = coop_closest<SLACK, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v, nullptr, coop_rl);
+        }
+        if (!ok) break;
+        int more = -1;
+        if (me == b && r >= 0 && t <= L.ray.max_t && t >= L.ray.min_t) {  // accel.h:133
+            const BsdfRecord& bb = bsdf_of(sc, __float_as_int(gld4(sc.shade + kShadeStride * static_cast<size_t>(r)).w));
+            if (is_delta(bb) && is_zero(ld3(bb.emission)) && L.c.steps + 1 <= (1 << 30)) {
+                ++L.c.steps;  // resolve(): one more query, the hit shaded
+                shade_hit(sc, r, u, v, t, L.ray.d, L.h);
+                const float dist2 = L.h.dist * L.h.dist;
+                BDPT_DIST_TO_GRAZE
+                const float absCosIn = fabsf(L.h.wo.z);
+#if BDPT_RING_AHEAD
+                if (L.rng.n + BDPT_RING_AHEAD >= 227 && !mt_ring_ahead(L.rng) && fr.diag) gadd(fr.diag + kDiagErrors, 1ull);
+#endif
+                L.c.vcm *= div_w(dist2, absCosIn);  // bdpt.h:193-209 / :73-136 (no connection at a delta vertex)
+                L.c.vc *= rcp_w(absCosIn);
+                L.c.rr = rr_probability(fr, L.c.depth, L.c.tp);
+                const bool light = L.state == ST_LIGHT;
+                const bool cont = continue_walk(bb, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, L.c.rr);
+                if (cont && walk_continues(L, fr)) {  // bdpt.h:188 / :68
+                    ri = ray_inv(L.ray, cull_near_for(L));
+                    more = ri.fast && !far_origin(sc, L.ray.o) && !(L.ray.min_t > L.ray.max_t) ? 1 : 2;
+                } else {
+                    if (light) L.state = ST_DEFER;  // the eye subpath starts next step
+                    else finish<false>(L, fr, fb, cnt);  // L.state = ST_IDLE
+                    more = 0;
+                }
+            }
+        }
+        more = __shfl(more, b);
+        if (more == 1) continue;
+        bounced = more;
+        break;
+    }
+    Lcaller.rng = L.rng, Lcaller.state = L.state, Lcaller.ray = L.ray, Lcaller.h = L.h;
+    ri_caller = ri;
+    return bounced;
+}
+#endif
+
 // One query for the lane's pending state, then the state advance.
 template <bool FULL, bool COUNT>
 __device__ __forceinline__ void step(Lane& L, const DevScene& sc, const DevFrame& fr, float* __restrict__ fb,
@@ -299,6 +374,19 @@ struct KParams {
 #if !BDPT_HELP
 #undef BDPT_HELP_BATCH
 #define BDPT_HELP_BATCH 0
+#endif
+#ifndef BDPT_HELP_CLOCKS
+#define BDPT_HELP_CLOCKS 0  // measurement only: the counting pass's stack-depth words carry the claim / completion / batch clocks
+#endif
+#ifndef BDPT_EXPRESS_CHAIN
+#define BDPT_EXPRESS_CHAIN 0  // RR build: a lone long walk's delta bounces back to back inside the express block
+#endif
+#ifndef BDPT_EXPRESS_PROBE
+#define BDPT_EXPRESS_PROBE 0  // measurement only (RR build): express waves with one busy lane, clocks per iteration and in the coop walk
+#endif
+#if BDPT_RR != 1
+#undef BDPT_EXPRESS_PROBE
+#define BDPT_EXPRESS_PROBE 0
 #endif
 #ifndef BDPT_HELP_SREG
 #define BDPT_HELP_SREG 1  // BDPT_HELP: the ring positions held in SGPRs during the walk loop (no LDS reads per iteration; 324.6 vs 322.7)
@@ -403,6 +491,10 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     // the trapped lane advances one bounce per walk instead of one per shared
     // shading step (the frame cannot end before it does).
     bool long_walk = false;
+#if BDPT_EXPRESS_PROBE
+    uint64_t xp_iters = 0, xp_coop = 0, xp_total = 0, xp_t = 0;  // (wave-uniform)
+    bool xp_prev = false;
+#endif
 #if BDPT_HELP
     // helping: the lane walks a task's shadow ray (tracing is set too) or, with BDPT_HELP_DEFER,
     // waits one iteration for its claimed record (hwait)
@@ -440,6 +532,17 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         const KParams* P = (const KParams*)(ConstKParams)pa;
         const uint64_t longs = BDPT_RR == 1 && BDPT_EXPRESS_DEPTH > 0 ? __ballot(long_walk) : 0ull;
         const bool express = longs != 0;  // wave-uniform
+#if BDPT_EXPRESS_PROBE
+        // express waves with one busy lane: iterations, their clocks, and the coop block's share
+        const bool xp_lone = express && popc64(__ballot(BDPT_BUSY(L.state))) == 1;
+        {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            if (xp_prev) xp_total += now - xp_t;
+            xp_t = now;
+            xp_prev = xp_lone;
+            if (xp_lone) xp_iters++;
+        }
+#endif
 #if BDPT_RR == 1
         if (BDPT_DIAG && BDPT_RR_DIAG && express && lane0() && P->fr.diag) {  // how many trapped walks share a wave (bdpt_stats)
             const int k = popc64(longs);
@@ -615,7 +718,15 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         // walks alone from the root; waiting lanes walk alone once the wave holds more
         // than BDPT_COOP_MAX busy lanes or leaves express mode (their walk restarts),
         // in their turn: a walk begun while another lane still walks alone waits too.
+#if BDPT_EXPRESS_PROBE
+        const uint64_t xc0 = __builtin_amdgcn_s_memtime();
+#endif
         if (!COUNT && express) {
+#if BDPT_ROOT_LDS
+            const RootLds* const coop_rl = root_in_lds ? &root_lds : nullptr;
+#else
+            const RootLds* const coop_rl = nullptr;
+#endif
             const uint64_t busy = __ballot(BDPT_BUSY(L.state)), wt = __ballot(coop_wait), bg = __ballot(began);
 #if BDPT_COOP_GROUPS
             if (!(P->fr.sched_flags & kSchedNoCoopGroups) && popc64(busy) >= 2 && popc64(busy) <= BDPT_COOP_MAX &&
@@ -649,12 +760,13 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 float t = 0.f, u = 0.f, v = 0.f;
                 int r = -1;
                 bool ok = coop_closest_groups<SLACK>(tsc, q, qi, bounded ? 2.f * guess : q.max_t, act, cs, gbase, cap, G,
-                                                     t, r, u, v);
+                                                     t, r, u, v, coop_rl);
                 const bool again = bounded && ok && r < 0;  // nothing below the bound: the walk unbounded
                 if (__ballot(again)) {
                     float t2 = 0.f, u2 = 0.f, v2 = 0.f;
                     int r2 = -1;
-                    const bool ok2 = coop_closest_groups<SLACK>(tsc, q, qi, q.max_t, again, cs, gbase, cap, G, t2, r2, u2, v2);
+                    const bool ok2 = coop_closest_groups<SLACK>(tsc, q, qi, q.max_t, again, cs, gbase, cap, G, t2, r2, u2, v2,
+                                                                coop_rl);
                     if (again) t = t2, u = u2, v = v2, r = r2, ok = ok2;
                 }
                 // each walk's owner takes its group's result (group = the owner's rank among the busy lanes)
@@ -676,26 +788,89 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
             if (popc64(busy) <= BDPT_COOP_MAX && (bg | wt) == busy) {
                 const int b = __ffsll(static_cast<unsigned long long>(wt ? wt : bg)) - 1;
                 const int me = static_cast<int>(opaque_tid() & 63);
-                Ray q;
-                q.o = mk(__shfl(L.ray.o.x, b), __shfl(L.ray.o.y, b), __shfl(L.ray.o.z, b));
-                q.d = mk(__shfl(L.ray.d.x, b), __shfl(L.ray.d.y, b), __shfl(L.ray.d.z, b));
-                q.min_t = __shfl(L.ray.min_t, b), q.max_t = __shfl(L.ray.max_t, b);
-                RayInv qi;
-                qi.inv = mk(__shfl(ri.inv.x, b), __shfl(ri.inv.y, b), __shfl(ri.inv.z, b));
-                qi.near = __shfl(ri.near, b);
-                qi.fast = true;
-                // the lane's last hit distance (Hit::dist, shade_hit), the bound's guess
-                const float guess = BDPT_GRAZE_IN_DIST ? -1.f : __shfl(L.h.dist, b);
                 const CoopStack cs{stack_mem + (threadIdx.x & ~63u), kBlock};
                 float t = 0.f, u = 0.f, v = 0.f;
                 int r = -1;
                 bool ok = true;
-                for (int pass = guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
-                    const float bound = pass == 0 ? 2.f * guess : q.max_t;
-                    ok = SLACK ? coop_closest<true, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v)
-                               : coop_closest<false, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v);
+                // A lone long walk (BDPT_EXPRESS_CHAIN): its delta bounces run here, back to
+                // back, each walked by the whole wave, until the chain reaches a vertex the
+                // sweep must shade — the loop top, the walk loop and the sweep's empty bodies
+                // took ~40 % of each bounce's clocks (round 6 probe, BDPT_EXPRESS_PROBE).
+                const bool chain = BDPT_EXPRESS_CHAIN && popc64(busy) == 1;
+                int bounced = -1;  // -1: the result goes to the sweep; 0: the chain ended here; 2: its next query begins at the loop top
+#if BDPT_EXPRESS_CHAIN == 2
+                if (chain) {
+                    bounced = express_chain<SLACK>(L, b, ri, P->sc, P->fr, P->fb, tsc, stack_mem + (threadIdx.x & ~63u),
+                                                   coop_rl, t, r, u, v, ok);
+                } else
+#endif
+                for (;;) {
+                    Ray q;
+                    q.o = mk(__shfl(L.ray.o.x, b), __shfl(L.ray.o.y, b), __shfl(L.ray.o.z, b));
+                    q.d = mk(__shfl(L.ray.d.x, b), __shfl(L.ray.d.y, b), __shfl(L.ray.d.z, b));
+                    q.min_t = __shfl(L.ray.min_t, b), q.max_t = __shfl(L.ray.max_t, b);
+                    RayInv qi;
+                    qi.inv = mk(__shfl(ri.inv.x, b), __shfl(ri.inv.y, b), __shfl(ri.inv.z, b));
+                    qi.near = __shfl(ri.near, b);
+                    qi.fast = true;
+                    // the lane's last hit distance (Hit::dist, shade_hit), the bound's guess
+                    const float guess = BDPT_GRAZE_IN_DIST ? -1.f : __shfl(L.h.dist, b);
+                    r = -1;
+                    ok = true;
+                    for (int pass = guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
+                        const float bound = pass == 0 ? 2.f * guess : q.max_t;
+                        ok = SLACK ? coop_closest<true, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v,
+                                                                         nullptr, coop_rl)
+                                   : coop_closest<false, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v,
+                                                                          nullptr, coop_rl);
+                    }
+                    if (BDPT_EXPRESS_CHAIN != 1 || !chain || !ok) break;
+                    int more = -1;  // (lane b) -1: not a delta bounce; 0: the chain ended; 1: next bounce here; 2: at the loop top
+                    if (me == b && r >= 0 && t <= L.ray.max_t && t >= L.ray.min_t) {  // accel.h:133
+                        const BsdfRecord& bb =
+                            bsdf_of(P->sc, __float_as_int(gld4(P->sc.shade + kShadeStride * static_cast<size_t>(r)).w));
+                        if (is_delta(bb) && is_zero(ld3(bb.emission)) && L.c.steps + 1 <= (1 << 30)) {
+                            // the sweep's work at a delta, non-emitting vertex: resolve() (one more
+                            // query, the hit shaded), the vertex update (bdpt.h:193-209 / :73-136, no
+                            // connection at a delta vertex), ContinuePathRandomWalk (bdpt.h:243-291)
+                            // and the loop test (bdpt.h:188 / :68)
+                            ++L.c.steps;
+                            shade_hit(P->sc, r, u, v, t, L.ray.d, L.h);
+                            const float dist2 = L.h.dist * L.h.dist;
+                            BDPT_DIST_TO_GRAZE
+                            const float absCosIn = fabsf(L.h.wo.z);
+#if BDPT_DEEP_RNG && BDPT_RING_AHEAD
+                            if (L.rng.n + BDPT_RING_AHEAD >= 227 && !mt_ring_ahead(L.rng) && P->fr.diag)
+                                gadd(P->fr.diag + kDiagErrors, 1ull);
+#endif
+                            L.c.vcm *= div_w(dist2, absCosIn);
+                            L.c.vc *= rcp_w(absCosIn);
+                            L.c.rr = rr_probability(P->fr, L.c.depth, L.c.tp);
+                            const bool light = L.state == ST_LIGHT;
+                            const bool cont = continue_walk(bb, L.h, L.rng, L.c.tp, L.c.depth, L.c.vc, L.c.vcm, L.ray, L.c.rr);
+                            if (cont && walk_continues(L, P->fr)) {
+                                ri = ray_inv(L.ray, cull_near_for(L));
+                                more = ri.fast && !far_origin(P->sc, L.ray.o) && !(L.ray.min_t > L.ray.max_t) ? 1 : 2;
+                            } else {
+                                if (light) L.state = ST_DEFER;  // the eye subpath starts next step
+                                else finish<false>(L, P->fr, P->fb, cnt);  // L.state = ST_IDLE
+                                more = 0;
+                            }
+                        }
+                    }
+                    more = __shfl(more, b);
+                    if (more == 1) continue;  // the next bounce's walk, by the whole wave
+                    bounced = more;
+                    break;
                 }
-                if (me == b) {
+                if (bounced >= 0) {  // lane b's bounces ran here: no result pending
+                    if (me == b) {
+                        coop_wait = false;
+                        tracing = false;
+                        has_res = false;
+                        long_walk = L.state != ST_IDLE && L.c.depth > P->fr.express_depth;
+                    }
+                } else if (me == b) {
                     coop_wait = false;
                     if (ok) {
                         res = r, rt = t, ru = u, rv = v;
@@ -721,6 +896,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         } else {
             coop_wait = false;
         }
+#if BDPT_EXPRESS_PROBE
+        if (xp_lone) xp_coop += __builtin_amdgcn_s_memtime() - xc0;
+#endif
 #endif
         const uint64_t c0 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
 #if BDPT_READY_HOIST
@@ -777,6 +955,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 help_begin(ri.near);
             }
 #endif
+            const uint64_t hk0 = COUNT && BDPT_HELP_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
             {
                 const TaskCtl ctl = task_ctl(L.c);
 #if BDPT_HELP_SREG
@@ -826,6 +1005,8 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     }
                 }
             }
+            if (COUNT && BDPT_HELP_CLOCKS && first_active_lane())  // (probe build: claim block clocks in stack_gt8)
+                cnt.c[16] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - hk0);
             tr = __ballot(tracing);
 #if BDPT_HELP_DEFER
             if (!tr && !__ballot(hfin) && !__ballot(hwait)) break;
@@ -878,6 +1059,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
             }
 #if BDPT_HELP
+            const uint64_t hk1 = COUNT && BDPT_HELP_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
             if (hfin) {  // the task's shadow ray: unoccluded -> its contribution to the pixel
                 helping = false;
                 if (ts.best < 0) {
@@ -891,6 +1073,8 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     }
                 }
             }
+            if (COUNT && BDPT_HELP_CLOCKS && first_active_lane())  // (probe build: completion clocks in stack_gt12)
+                cnt.c[17] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - hk1);
 #endif
         }
         const uint64_t c1 = COUNT ? __builtin_amdgcn_s_memtime() : 0;
@@ -919,7 +1103,10 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #if BDPT_HELP_BATCH
         // the connections of the eye vertices reached in this step, over the whole wave
         if (__ballot(shade_now)) {
+            const uint64_t hk2 = COUNT && BDPT_HELP_CLOCKS ? __builtin_amdgcn_s_memtime() : 0;
             conn_batch<COUNT>(L, shade_now && act2 == A_CONN && P->fr.strategy == 0, P->sc, P->fr, ls, cnt);
+            if (COUNT && BDPT_HELP_CLOCKS && first_active_lane())  // (probe build: batch clocks in stack_gt16)
+                cnt.c[18] += static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - hk2);
             if (shade_now) advance<COUNT, 2>(L, act2, P->sc, P->fr, P->fb, ls, cnt);
         }
 #endif
@@ -943,6 +1130,13 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         for (int k = 0; k < BDPT_EYE_SLOTS; k++) eye_slot_reset(kp.fb, k, -1);
 #endif
     if (BDPT_DIAG && lane0() && kpp->fr.diag) gmax(kpp->fr.diag + kDiagEnd, __builtin_amdgcn_s_memrealtime());
+#if BDPT_EXPRESS_PROBE
+    if (lane0() && xp_iters) {  // into bdpt_stats.sched (a timed run writes nothing else there)
+        gadd(kpp->counters + kCounters + 3, static_cast<unsigned long long>(xp_iters));
+        gadd(kpp->counters + kCounters + 3 + 1, static_cast<unsigned long long>(xp_coop));
+        gadd(kpp->counters + kCounters + 3 + 2, static_cast<unsigned long long>(xp_total));
+    }
+#endif
 #if BDPT_TAIL_PROBE && BDPT_RR != 1
     // longest drain with <= 4 busy lanes, longest drain, their sum over waves, waves that had one
     if (lane0() && kpp->fr.diag) {

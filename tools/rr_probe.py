@@ -52,6 +52,9 @@ for flags, label in passes:
            "parked": st.get("parked_samples"), "launches": st.get("launches"),
            "long_walks_max": st.get("rr_long_walks_max"), "express_iters_1_2to4_more": st.get("rr_express_iters"),
            "wall_s": round(time.time() - t, 3),
+           # BDPT_EXPRESS_PROBE builds: express iterations with one busy lane, their clocks in the
+           # cooperative walk block, and in the whole loop iteration (bdpt_stats.sched)
+           "sched": st.get("sched"),
            "kernel": st["kernel"]}
     if flags:
         out.update(max_light_depth=st["max_light_depth"], max_eye_depth=st["max_eye_depth"],
