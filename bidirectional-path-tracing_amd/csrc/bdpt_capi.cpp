@@ -59,6 +59,14 @@ int frame_kernel_blocks_per_cu_rr(size_t dyn_lds);
 hipError_t launch_chain_rr(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
                            uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
                            hipStream_t stream, void* dparams);
+// bdpt_kernels_rrc.hip: the Russian-roulette megakernel for scenes with glass (lone trapped chains inline)
+hipError_t launch_frame_rrc(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                            uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
+                            hipStream_t stream, void* dparams);
+int frame_kernel_blocks_per_cu_rrc(size_t dyn_lds);
+hipError_t launch_chain_rrc(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf, uint2* gstack,
+                            uint32_t nslots, unsigned long long* work, unsigned long long* counters, int grid,
+                            hipStream_t stream, void* dparams);
 // bdpt_kernels_split.hip: the same megakernel for short subpaths (no ST_DEFER step)
 hipError_t launch_frame_split(const dev::DevScene& sc, const dev::DevFrame& fr, float* fb, float* lvbuf,
                               uint2* gstack, uint32_t nslots, unsigned long long* work, unsigned long long* counters,
@@ -218,6 +226,7 @@ struct bdpt_ctx {
     uint32_t* park = nullptr;     // Russian roulette: continuation records + parked-slot list (DevFrame::park)
     float4* tasks = nullptr;      // per-wave shadow-ray task rings (DevFrame::tasks; read by BDPT_HELP builds)
     uint32_t task_cap = 0;        // their capacity (tasks per wave, a power of two)
+    bool has_glass = false;       // a GlassBSDF material: Russian-roulette renders run bdpt_kernels_rrc.hip
     int32_t* row_order = nullptr;  // bdpt_set_row_order (device copy; DevFrame::row_order)
     int32_t row_order_n = 0;       // its row count (0: top to bottom)
     unsigned long long* row_cost = nullptr;  // counting renders: queries per local row (DevFrame::row_cost)
@@ -570,6 +579,7 @@ int bdpt_ctx_create(const bdpt_scene* s, int32_t hip_device, bdpt_ctx** out) {
     {
         const std::vector<BsdfRecord> dev_bsdfs = device_bsdfs(L.bsdfs);
         if ((rc = upload(c.get(), dev_bsdfs.data(), dev_bsdfs.size() * sizeof(BsdfRecord), &p))) return rc;
+        for (const BsdfRecord& b : dev_bsdfs) c->has_glass = c->has_glass || b.kind == BSDF_GLASS;
     }
     c->sc.bsdf = static_cast<const BsdfRecord*>(p);
     if ((rc = upload(c.get(), L.emitters.data(), L.emitters.size() * sizeof(EmitterRecord), &p))) return rc;
@@ -848,7 +858,13 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
     int64_t launches = 0;
     if (fr.total_samples > 0) {
         if (rr) {  // never more resident blocks than the slots allocated
-            const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_rr(
+            // scenes with a dielectric can trap a subpath in a chain of delta bounces: the
+            // build that runs a lone chain inline (bdpt_kernels_rrc.hip); BDPT_RR_CHAIN=0/1 forces
+            const char* ce = std::getenv("BDPT_RR_CHAIN");
+            const bool chain = ce ? *ce == '1' : c->has_glass;
+            auto launch_rr = chain ? launch_frame_rrc : launch_frame_rr;
+            auto launch_chain_k = chain ? launch_chain_rrc : launch_chain_rr;
+            const int grid = std::min(c->grid, c->cus * (chain ? frame_kernel_blocks_per_cu_rrc : frame_kernel_blocks_per_cu_rr)(
                                                            4 * static_cast<size_t>(c->sc.lds_words)));
             const int park_depth = park_depth_setting();
             const bool park = park_depth > 0 && !(p->flags & BDPT_FLAG_COUNT);
@@ -860,21 +876,19 @@ int bdpt_render(bdpt_ctx* c, const bdpt_frame_params* p, float* fb, void* hip_st
                 fr.park_depth = park_depth;
                 fr.park_flags = dev::kParkOn;
             }
-            HIP_TRY(launch_frame_rr(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
-                                    c->dparams));
+            HIP_TRY(launch_rr(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st, c->dparams));
             const int rounds = park ? park_rounds_setting() : 0;
             uint32_t* const list = c->park + static_cast<size_t>(c->nslots) * kParkSlotWords;
             for (int k = 0; k < rounds; k++) {
-                HIP_TRY(launch_chain_rr(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, kChainGrid, st,
-                                        c->dparams));
+                HIP_TRY(launch_chain_k(sc, fr, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, kChainGrid, st,
+                                       c->dparams));
                 HIP_TRY(hipMemsetAsync(list, 0, sizeof(uint32_t), st));  // the resume launch parks anew
                 dev::DevFrame fres = fr;
                 fres.park_flags = dev::kParkResume | (k + 1 < rounds ? dev::kParkOn : 0u);
-                HIP_TRY(launch_frame_rr(sc, fres, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st,
-                                        c->dparams));
+                HIP_TRY(launch_rr(sc, fres, fb, c->lv, c->gstack, c->nslots, c->work, c->counters, grid, st, c->dparams));
             }
             launches += 2 * rounds;
-            c->last_kernel = "bdpt_frame_kernel_rr";
+            c->last_kernel = chain ? "bdpt_frame_kernel_rrc" : "bdpt_frame_kernel_rr";
         } else if (p->rr_depth > kLazyRrDepth) {  // never more resident blocks than the slots allocated
             const int grid = std::min(c->grid, c->cus * frame_kernel_blocks_per_cu_deep(
                                                            4 * static_cast<size_t>(c->sc.lds_words)));

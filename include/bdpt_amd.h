@@ -290,7 +290,8 @@ int bdpt_render_sample(bdpt_ctx* ctx, const bdpt_frame_params* params, const flo
 int bdpt_get_stats(bdpt_ctx* ctx, bdpt_stats* out);
 /* (new) The frame-kernel build the context's last bdpt_render launched: "bdpt_frame_kernel",
  * "_split" (rrDepth <= 3: no deferred shading step between the subpaths), "_deep" (rrDepth > 28),
- * "_rr" (Russian roulette) or "_hbm" (BSDF records in HBM); "" before the first render. For
+ * "_rr" (Russian roulette), "_rrc" (Russian roulette in a scene with glass: a lone subpath trapped by
+ * total internal reflection bounces inline) or "_hbm" (BSDF records in HBM); "" before the first render. For
  * matching profiler records to the kernel that ran. */
 const char* bdpt_last_kernel(const bdpt_ctx* ctx);
 /* Waits for all work queued by this context (on every stream it was given). */

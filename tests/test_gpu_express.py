@@ -21,18 +21,22 @@ from test_gpu_parity import TOL, report, rr_integrator
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("chain", ["1", "0"])
 @pytest.mark.parametrize("groups", ["1", "0"])
 @pytest.mark.parametrize("depth", ["3", "12"])
 @pytest.mark.parametrize("name", ["R1_caustic_rr_64x64_spp16", "R2_hardlight_rr_64x64_spp16",
                                   "R6_caustic_rr_512x512_spp2_rows32"])
-def test_gpu_express_walks_match_reference_golden(name, depth, groups, golden_manifest, monkeypatch):
+def test_gpu_express_walks_match_reference_golden(name, depth, groups, chain, golden_manifest, monkeypatch):
+    """chain: the build that runs a lone walk's delta bounces inline (bdpt_kernels_rrc.hip, chosen for
+    scenes with glass) or the plain RR build, forced either way (BDPT_RR_CHAIN)."""
     monkeypatch.setenv("BDPT_EXPRESS_DEPTH", depth)
     monkeypatch.setenv("BDPT_COOP_GROUPS", groups)
+    monkeypatch.setenv("BDPT_RR_CHAIN", chain)
     m = golden_manifest["rr_framebuffers"][name]
     it = rr_integrator(m["scene"], m["width"], m["height"], m["spp"], m["rr_depth"])
     fb = it.render_frame(row_offset=0, row_stride=m["row_stride"]).reshape(-1)
     st = it.stats()
-    assert st["kernel"].endswith("_rr"), st["kernel"]
+    assert st["kernel"] == ("bdpt_frame_kernel_rrc" if chain == "1" else "bdpt_frame_kernel_rr"), st["kernel"]
     assert st["capped_samples"] == 0 and st["schedule_errors"] == 0
     # express waves ran, with one and with 2-4 long walks at once
     assert st["rr_long_walks_max"] >= 2, st

@@ -12,7 +12,7 @@ NAME=$1; shift
 O=lib/obj_$NAME
 mkdir -p $O
 F="--offload-arch=gfx950 ${OPT:--O3} -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -I../include -Icsrc"
-if [ "${ALL:-0}" = "1" ]; then TUS="bdpt_kernels bdpt_kernels_deep bdpt_kernels_hbm bdpt_kernels_rr bdpt_kernels_split pt_kernels sample_state kat_kernels"
+if [ "${ALL:-0}" = "1" ]; then TUS="bdpt_kernels bdpt_kernels_deep bdpt_kernels_hbm bdpt_kernels_rr bdpt_kernels_rrc bdpt_kernels_split pt_kernels sample_state kat_kernels"
 else TUS="bdpt_kernels bdpt_kernels_split"; fi
 # HOST=1: the C-ABI translation units too (layout switches the upload must follow)
 if [ "${HOST:-0}" = "1" ]; then TUS="$TUS bdpt_capi bdpt_multi"; fi

@@ -18,6 +18,8 @@
 #                                             BASELINE workloads, then every bench line, each bench
 #                                             under rocprofv3 --kernel-trace --stats, so a line and its
 #                                             kernel CSV come from the same run
+#   run.sh final_a LABEL / final_b LABEL      the same in two calls (a call is limited to 20 minutes):
+#                                             suite + smoke + PMC profiles, then the bench lines
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
@@ -87,20 +89,22 @@ ab)
 profile)
   timeout -k 10 900 bash tools/profile_round.sh $LABEL "$@"
   ;;
-final)
+final|final_a|final_b)
   P=gpurun_out/prof_$LABEL
   kt() {  # name limit bench args...: the bench line under the kernel trace
     local name=$1 lim=$2; shift 2
     echo "$lim ${LABEL}_bench_$name.json -- rocprofv3 --kernel-trace --stats -d $P/kt_$name -o kt --output-format csv -- python3 bench.py $*"
   }
-  tools/gpu_steps.sh \
+  A=( \
     "500 ${LABEL}_gpu_tests.log -- python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
     "120 ${LABEL}_smoke.log -- python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
     "300 ${LABEL}_prof_caustic.log -- bash tools/profile_round.sh $LABEL caustic 512 512 256" \
     "300 ${LABEL}_prof_hl.log -- bash tools/profile_round.sh $LABEL hardlight 512 512 1024" \
     "400 ${LABEL}_prof_c1024.log -- bash tools/profile_round.sh $LABEL caustic 1024 1024 1024" \
     "500 ${LABEL}_prof_synth.log -- bash tools/profile_round.sh $LABEL synth1m 2048 2048 512" \
-    "30 ${LABEL}_copy.log -- cp $P/pmc_*.json profiles/ && ls -la profiles/pmc_*" \
+    "30 ${LABEL}_copy.log -- cp $P/pmc_*.json profiles/ && ls -la profiles/pmc_*" )
+  # (final_b on another box: copy gpurun_out/prof_LABEL/pmc_*.json into profiles/ first, locally)
+  B=( \
     "$(kt caustic_512x512_256spp 250 --steps 20 --warmup 2)" \
     "$(kt hardlight_512x512_1024spp 250 --scene hardlight --spp 1024 --steps 5 --warmup 1)" \
     "$(kt caustic_1024x1024_1024spp 300 --width 1024 --height 1024 --spp 1024 --steps 1 --warmup 1)" \
@@ -109,7 +113,12 @@ final)
     "$(kt direct_caustic_512x512_64spp 150 --integrator direct --spp 64 --steps 5 --warmup 1)" \
     "200 ${LABEL}_tail.log -- python3 tools/shard_tail.py caustic 512 512 256 1 8" \
     "$(kt rr_hardlight_512x512_1024spp 250 --russian-roulette --scene hardlight --spp 1024 --steps 2 --warmup 1 --count-spp 16)" \
-    "$(kt rr_caustic_512x512_256spp 420 --russian-roulette --steps 1 --warmup 0)"
+    "$(kt rr_caustic_512x512_256spp 420 --russian-roulette --steps 1 --warmup 0)" )
+  case $MODE in
+  final) tools/gpu_steps.sh "${A[@]}" "${B[@]}" ;;
+  final_a) tools/gpu_steps.sh "${A[@]}" ;;
+  final_b) tools/gpu_steps.sh "${B[@]}" ;;
+  esac
   ;;
 *)
   echo "usage: run.sh tests|abtest|ab|profile|final LABEL ..." >&2
