@@ -391,6 +391,9 @@ struct KParams {
 #ifndef BDPT_HELP_SREG
 #define BDPT_HELP_SREG 1  // BDPT_HELP: the ring positions held in SGPRs during the walk loop (no LDS reads per iteration; 324.6 vs 322.7)
 #endif
+#ifndef BDPT_HELP_HOIST
+#define BDPT_HELP_HOIST 0  // BDPT_HELP: a claim's record loads issued before the lane's own hit is shaded
+#endif
 #ifndef BDPT_HELP_DEFER
 #define BDPT_HELP_DEFER 0  // BDPT_HELP: a claimed task's walk begins one walk iteration after its record loads (305.8 vs 323.5: not kept)
 #endif
@@ -979,12 +982,19 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     qhead = head + n;
 #endif
                     if (cand && rank < n) {
+#if !BDPT_HELP_HOIST
                         if (has_res) help_compact(L, res, rt, ru, rv, P->sc);  // frees L.ray
+#endif
                         const uint32_t slot = (head + rank) & (P->fr.task_cap - 1);
                         float4* const ring = task_ring(P->fr);
                         const uint32_t cap = P->fr.task_cap;
                         const float4 a = gld4(task_vec(ring, cap, slot, 0)), b = gld4(task_vec(ring, cap, slot, 1)),
                                      c = gld4(task_vec(ring, cap, slot, 2));
+#if BDPT_HELP_HOIST
+                        // the record's loads are in flight while the lane's own hit is shaded
+                        // (one exposed latency per claim round instead of two)
+                        if (has_res) help_compact(L, res, rt, ru, rv, P->sc);  // frees L.ray
+#endif
                         if (COUNT) cnt.q[3]++;  // (counting pass: claims)
                         L.ray = Ray{xyz(a), xyz(b), kEpsilon, a.w};
                         helping = true;

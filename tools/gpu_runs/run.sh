@@ -18,8 +18,10 @@
 #                                             BASELINE workloads, then every bench line, each bench
 #                                             under rocprofv3 --kernel-trace --stats, so a line and its
 #                                             kernel CSV come from the same run
-#   run.sh final_a LABEL / final_b LABEL      the same in two calls (a call is limited to 20 minutes):
-#                                             suite + smoke + PMC profiles, then the bench lines
+#   run.sh final_a / final_c / final_b LABEL  the same in three calls (a call is limited to 20 minutes):
+#                                             suite + smoke + the 512^2 PMC profiles; the 1024^2 and
+#                                             synth1m profiles; the bench lines (copy each call's
+#                                             gpurun_out/prof_LABEL/pmc_*.json into profiles/ between)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
@@ -89,7 +91,7 @@ ab)
 profile)
   timeout -k 10 900 bash tools/profile_round.sh $LABEL "$@"
   ;;
-final|final_a|final_b)
+final|final_a|final_b|final_c)
   P=gpurun_out/prof_$LABEL
   kt() {  # name limit bench args...: the bench line under the kernel trace
     local name=$1 lim=$2; shift 2
@@ -99,10 +101,11 @@ final|final_a|final_b)
     "500 ${LABEL}_gpu_tests.log -- python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
     "120 ${LABEL}_smoke.log -- python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
     "300 ${LABEL}_prof_caustic.log -- bash tools/profile_round.sh $LABEL caustic 512 512 256" \
-    "300 ${LABEL}_prof_hl.log -- bash tools/profile_round.sh $LABEL hardlight 512 512 1024" \
+    "300 ${LABEL}_prof_hl.log -- bash tools/profile_round.sh $LABEL hardlight 512 512 1024" )
+  C=( \
     "400 ${LABEL}_prof_c1024.log -- bash tools/profile_round.sh $LABEL caustic 1024 1024 1024" \
-    "500 ${LABEL}_prof_synth.log -- bash tools/profile_round.sh $LABEL synth1m 2048 2048 512" \
-    "30 ${LABEL}_copy.log -- cp $P/pmc_*.json profiles/ && ls -la profiles/pmc_*" )
+    "500 ${LABEL}_prof_synth.log -- bash tools/profile_round.sh $LABEL synth1m 2048 2048 512" )
+  CP=( "30 ${LABEL}_copy.log -- cp $P/pmc_*.json profiles/ && ls -la profiles/pmc_*" )
   # (final_b on another box: copy gpurun_out/prof_LABEL/pmc_*.json into profiles/ first, locally)
   B=( \
     "$(kt caustic_512x512_256spp 250 --steps 20 --warmup 2)" \
@@ -115,8 +118,9 @@ final|final_a|final_b)
     "$(kt rr_hardlight_512x512_1024spp 250 --russian-roulette --scene hardlight --spp 1024 --steps 2 --warmup 1 --count-spp 16)" \
     "$(kt rr_caustic_512x512_256spp 420 --russian-roulette --steps 1 --warmup 0)" )
   case $MODE in
-  final) tools/gpu_steps.sh "${A[@]}" "${B[@]}" ;;
+  final) tools/gpu_steps.sh "${A[@]}" "${C[@]}" "${CP[@]}" "${B[@]}" ;;
   final_a) tools/gpu_steps.sh "${A[@]}" ;;
+  final_c) tools/gpu_steps.sh "${C[@]}" ;;
   final_b) tools/gpu_steps.sh "${B[@]}" ;;
   esac
   ;;
