@@ -412,7 +412,20 @@ struct KParams {
 // "this is lane 0" from an opaque threadIdx.x (lanes_below: bdpt_device.hpp).
 __device__ __forceinline__ bool lane0() { return (opaque_tid() & 63) == 0; }
 #ifndef BDPT_TAIL_CHUNK
-#define BDPT_TAIL_CHUNK 4  // x the grid's lanes from the end: finer claims (0: 64-sample chunks throughout)
+#define BDPT_TAIL_CHUNK 4  // 0: 64-sample chunks throughout; else finer claims near the end (below)
+#endif
+// Where the finer claims begin, in quarters of the grid's lanes from the frame's end:
+// 16-sample claims from BDPT_TAIL_Z16 / 4 x lanes, 4-sample ones from BDPT_TAIL_Z4 / 4 x
+// lanes. Round 6 re-measured them on the task build (each claim seeds a whole wave's
+// generators, so finer claims cost throughput): 16 / 8 / 4 quarters with the 4-sample
+// claims from 2: Caustic 325.2 / 325.6 / 327.8 Msamples/s, the 1/8 row shard's kernel
+// efficiency 0.951 / 0.958-0.965 / 0.961-0.969 and, two frames in flight, 0.957 / 0.975
+// / 0.981 (profiles/round6_r6s_tail.log)
+#ifndef BDPT_TAIL_Z16
+#define BDPT_TAIL_Z16 4
+#endif
+#ifndef BDPT_TAIL_Z4
+#define BDPT_TAIL_Z4 2
 #endif
 #ifndef BDPT_CLAIM_SCALAR
 #define BDPT_CLAIM_SCALAR 1  // the claimed chunk base broadcast by readfirstlane (scalar) instead of a shuffle
@@ -421,7 +434,7 @@ __device__ __forceinline__ bool lane0() { return (opaque_tid() & 63) == 0; }
 __device__ __forceinline__ uint64_t tail_chunk(uint64_t last_base, uint64_t total) {
     if (!BDPT_TAIL_CHUNK) return 64;
     const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * kBlock;
-    return last_base + BDPT_TAIL_CHUNK * lanes < total ? 64 : last_base + lanes / 2 < total ? 16 : 4;
+    return last_base + BDPT_TAIL_Z16 * lanes / 4 < total ? 64 : last_base + BDPT_TAIL_Z4 * lanes / 4 < total ? 16 : 4;
 }
 
 template <bool FULL, bool COUNT, bool SLACK>
@@ -570,7 +583,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 // Near the frame's end a wave's unstarted chunk samples wait for
                 // its busy lanes (up to a whole sample's latency) while other
                 // waves run dry: once the claims seen by this wave come within
-                // BDPT_TAIL_CHUNK x the grid's lanes of the end, claim 16, then
+                // BDPT_TAIL_Z16 / 4 x the grid's lanes of the end, claim 16, then
                 // 4 samples at a time (any sizes partition [0, total)).
                 const uint64_t want = tail_chunk(chunk_base, total);
                 unsigned long long base = 0;
