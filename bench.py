@@ -250,13 +250,14 @@ def main() -> None:
                          "1 emitter + 1 BSDF sample) on the same substrate, for comparison")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the in-run parity check of the GPU row shard against the CPU reference frame")
-    ap.add_argument("--pipeline", type=int, default=2,
-                    help="BDPT frames in flight: 1 = each step waits for its frame; 2 (default) = consecutive "
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="BDPT frames in flight: 1 (default) = each step waits for its frame; 2 = consecutive "
                          "steps' frames overlap (two contexts, streams and framebuffers): the next frame's blocks "
                          "start on the CUs the previous frame's draining blocks leave, hiding most of the "
                          "persistent grid's end tail, which each of N ranks pays per frame (1/8 row shard: 0.961 "
                          "-> 0.981 of full/8, DESIGN.md §5). Every frame is still rendered whole, into its own "
-                         "framebuffer, and reduced; the clock brackets all K steps")
+                         "framebuffer, and reduced; the clock brackets all K steps. (Each launch's event time then "
+                         "includes the overlap with its neighbour, so it exceeds the per-step time.)")
     ap.add_argument("--profiles", default=os.path.join(REPO, "profiles"),
                     help="directory of kernel-build-stamped PMC summaries (pmc_<workload>.json, "
                          "pmc_deep_<workload>.json) for roofline.traffic / limiter")
