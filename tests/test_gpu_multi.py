@@ -153,9 +153,10 @@ def test_gpu_cli_devices_flag(golden_manifest, tmp_path):
     assert np.allclose(img, ref, rtol=2 ** -10, atol=0)
 
 
-def test_gpu_bench_two_rank_rehearsal(tmp_path):
+@pytest.mark.parametrize("pipeline", ["1", "2"])
+def test_gpu_bench_two_rank_rehearsal(tmp_path, pipeline):
     """bench.py's N > 1 path (torch.distributed.run, one rank per device, barrier +
-    max-over-ranks timing, row shards, the framebuffer reduce, rank 0's JSON line)
+    max-over-ranks timing, row shards, the framebuffer reduce, rank 0's JSON line), one and two frames in flight,
     rehearsed on this one-GPU box: BDPT_BENCH_REHEARSAL=1 puts both ranks on GPU 0
     and reduces over gloo instead of RCCL."""
     import json
@@ -164,8 +165,8 @@ def test_gpu_bench_two_rank_rehearsal(tmp_path):
     env = dict(os.environ, BDPT_BENCH_REHEARSAL="1", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "1", "--warmup", "1", "--width", "64", "--height", "64", "--spp", "4",
-           "--no-cpu"]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--width", "64", "--height", "64", "--spp", "4",
+           "--no-cpu", "--pipeline", pipeline]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -174,5 +175,8 @@ def test_gpu_bench_two_rank_rehearsal(tmp_path):
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["samples_per_step"] == 64 * 64 * 4
     rk = out["ranks"]  # what a scaling run needs to be diagnosed
     assert rk["world_size"] == 2 and rk["backend"] == "gloo" and rk["rehearsal_one_device"]
-    assert len(rk["kernel_ms"]) == 2 and min(rk["kernel_ms"]) > 0 and len(rk["reduce_ms"]) == 2
+    assert len(rk["kernel_ms"]) == 2 and min(rk["kernel_ms"]) > 0
+    assert out["config"]["frames_in_flight"] == int(pipeline)
+    if pipeline == "1":  # (frames in flight: the reduce runs on the frame's stream, untimed)
+        assert len(rk["reduce_ms"]) == 2
     assert sum(rk["samples"]) == 64 * 64 * 4 and rk["kernel_ms_max"] >= rk["kernel_ms_min"]
