@@ -18,7 +18,8 @@
 #                                             BASELINE workloads, then every bench line, each bench
 #                                             under rocprofv3 --kernel-trace --stats, so a line and its
 #                                             kernel CSV come from the same run
-#   run.sh final_a / final_c / final_b LABEL  the same in three calls (a call is limited to 20 minutes):
+#   run.sh final_a / final_c / final_b LABEL  the same in three calls (a call is limited to 20 minutes;
+#                                             final_tc = final_a's suite + smoke, then final_c):
 #                                             suite + smoke + the 512^2 PMC profiles; the 1024^2 and
 #                                             synth1m profiles; the bench lines (copy each call's
 #                                             gpurun_out/prof_LABEL/pmc_*.json into profiles/ between)
@@ -91,7 +92,7 @@ ab)
 profile)
   timeout -k 10 900 bash tools/profile_round.sh $LABEL "$@"
   ;;
-final|final_a|final_b|final_c)
+final|final_a|final_b|final_c|final_tc)
   P=gpurun_out/prof_$LABEL
   kt() {  # name limit bench args...: the bench line under the kernel trace
     local name=$1 lim=$2; shift 2
@@ -121,6 +122,7 @@ final|final_a|final_b|final_c)
   final) tools/gpu_steps.sh "${A[@]}" "${C[@]}" "${CP[@]}" "${B[@]}" ;;
   final_a) tools/gpu_steps.sh "${A[@]}" ;;
   final_c) tools/gpu_steps.sh "${C[@]}" ;;
+  final_tc) tools/gpu_steps.sh "${A[0]}" "${A[1]}" "${C[@]}" ;;  # (suite + smoke, then final_c)
   final_b) tools/gpu_steps.sh "${B[@]}" ;;
   esac
   ;;
