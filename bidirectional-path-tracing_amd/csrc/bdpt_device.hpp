@@ -902,6 +902,23 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
                                                       __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
 }
 
+// Lane i's value in every lane, for a wave-uniform i: v_readlane (a scalar
+// result, a few cycles) where __shfl's ds_bpermute takes an LDS round trip
+// (BDPT_READLANE; 0 keeps the shuffles). The value is the lane's register whether
+// or not it is active.
+#ifndef BDPT_READLANE
+#define BDPT_READLANE 1
+#endif
+#if BDPT_READLANE
+__device__ __forceinline__ int lane_val(int x, int i) { return __builtin_amdgcn_readlane(x, i); }
+__device__ __forceinline__ float lane_val(float x, int i) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), i));
+}
+#else
+__device__ __forceinline__ int lane_val(int x, int i) { return __shfl(x, i); }
+__device__ __forceinline__ float lane_val(float x, int i) { return __shfl(x, i); }
+#endif
+
 // SIMD-efficiency probe: true on the lowest active lane of the wave only.
 __device__ __forceinline__ bool first_active_lane() {
     return (__lane_id()) == static_cast<unsigned>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1);
@@ -1520,12 +1537,124 @@ struct CoopStack {
 // LDS instead of waiting on two dependent loads (BDPT_COOP_ROOT_LDS).
 struct RootLds;
 __device__ __forceinline__ WNode coop_node(const TravScene& sc, uint32_t link, const RootLds* rl);
+#ifndef BDPT_COOP_CP
+#define BDPT_COOP_CP 1  // coop_closest walks 16 entries per round, one child box / leaf triangle per lane (coop_closest_cp)
+#endif
+#if BDPT_COOP_CP && !BDPT_QNODES
+// coop_closest with the work of an entry spread over 4 lanes: each round pops up
+// to 16 entries, and lane 4s + c takes child c of entry s (its six planes and its
+// link: seven dword loads instead of the node's seven 16-byte vectors) or the
+// leaf's triangles c, c + 4 — one box or triangle test per lane where the
+// 64-entry round ran four box tests, a sort and up to four triangle tests in every
+// busy lane. A lone walk's frontier rarely holds more than 16 entries, and a
+// round of one wave alone on its SIMD costs its instructions, not its loads. The
+// per-child test is node_child_keys' (slab_fast with the slack, slab_fma without;
+// the same culls), the per-triangle acceptance coop_leaf's, so the result is the
+// same minimum (t, index) over the same candidates; entries are pushed unsorted
+// (the visiting order does not enter the result).
+// A lane's share of a cooperative walk's entry `link` (coop_closest_cp): child c
+// of an interior node — node_child_keys' test of that child, its entry distance
+// and link in (key, lnk) when the walk must visit it — or triangles c, c + 4 of a
+// leaf, with coop_leaf's acceptance rule against (lt, lb).
+template <bool SLACK>
+__device__ __forceinline__ void coop_entry_cp(const TravScene& sc, const Ray& r, const RayInv& ri, f3 oi, float far,
+                                              uint32_t link, int c, float& lt, int& lb, float& lu, float& lv,
+                                              float& key, uint32_t& lnk) {
+    if (link & kLeafBit) {
+        const uint32_t start = (link >> 3) & 0x0fffffffu, count = link & 7u;
+        Counts cnt;  // (not a counting pass)
+        for (uint32_t j = static_cast<uint32_t>(c); j < count; j += 4) {
+            const float4* p = sc.wtri + 3 * static_cast<size_t>(start + j);
+            const float4 q0 = gld4(p), q1 = gld4(p + 1), q2 = gld4(p + 2);
+            float t, u, v;
+            if (!tri_test_edges(xyz(q0), xyz(q1), xyz(q2), r, t, u, v)) continue;
+            const int idx = __float_as_int(q0.w);
+            if ((t < lt || (t == lt && lb >= 0 && idx < lb)) &&
+                ref_leaf_passes<false>(sc.lbox, __float_as_uint(q1.w), r, ri, cnt))
+                lt = t, lb = idx, lu = u, lv = v;
+        }
+    } else {
+        // child c of the 128-byte record: lo.x hi.x lo.y hi.y lo.z hi.z links, four floats each
+        const float* nd = reinterpret_cast<const float*>(sc.wnodes + kNodeStride * static_cast<size_t>(link)) + c;
+        const float clx = gld1(nd), chx = gld1(nd + 4), cly = gld1(nd + 8), chy = gld1(nd + 12), clz = gld1(nd + 16),
+                    chz = gld1(nd + 20);
+        const uint32_t l = __float_as_uint(gld1(nd + 24));
+        float tn, tf;
+        int d = kSlabHit;
+        if (SLACK || !BDPT_SLAB_FMA) d = slab_fast(clx, cly, clz, chx, chy, chz, r.o, ri.inv, tn, tf);
+        else slab_fma(clx, cly, clz, chx, chy, chz, oi, ri.inv, tn, tf);
+        const bool pass = SLACK ? d != kSlabMiss : !(tn > tf);
+        if (l != kEmptyLinkDev && pass && !(tn > far) && !(tf < ri.near)) key = tn, lnk = l;
+    }
+}
+#ifndef BDPT_COOP_CP_CALL
+#define BDPT_COOP_CP_CALL 0  // 1: coop_closest_cp out of line (its registers not part of the caller's allocation)
+#endif
+#if BDPT_COOP_CP_CALL
+#define BDPT_COOP_CP_INLINE __noinline__
+#else
+#define BDPT_COOP_CP_INLINE __forceinline__
+#endif
+template <bool SLACK>
+__device__ BDPT_COOP_CP_INLINE bool coop_closest_cp(const TravScene& sc, const Ray& r, const RayInv& ri, float bound,
+                                                CoopStack stk, int cap, float& best_t, int& best, float& best_u,
+                                                float& best_v, uint32_t* rounds) {
+    const uint32_t lane = __lane_id();
+    const int slot = static_cast<int>(lane >> 2), c = static_cast<int>(lane & 3u);
+    const f3 oi = SLACK || !BDPT_SLAB_FMA ? mk(0.f, 0.f, 0.f) : slab_fma_origin(r.o, ri.inv);
+    best_t = bound < r.max_t ? bound : r.max_t, best = -1, best_u = best_v = 0.f;
+    if (lane == 0) *stk.at(0) = u32x2{sc.wroot_link, __float_as_uint(-__builtin_inff())};
+    int sp = 1;
+    bool ok = true;
+    while (sp > 0) {
+        if (rounds) (*rounds)++;
+        const int k = sp < 16 ? sp : 16;
+        u32x2 e = {kEmptyLinkDev, 0u};
+        if (slot < k) e = *stk.at(sp - k + slot);
+        sp -= k;
+        const float far = cull_far(best_t);
+        const bool live = e.x != kEmptyLinkDev && !(__uint_as_float(e.y) > far);
+        float lt = best_t, lu = best_u, lv = best_v;
+        int lb = best;
+        float key = __builtin_inff();
+        uint32_t lnk = kEmptyLinkDev;
+        if (live) coop_entry_cp<SLACK>(sc, r, ri, oi, far, e.x, c, lt, lb, lu, lv, key, lnk);
+        // the wave's lexicographic minimum of (t, index) over the lanes that found a better hit
+        uint64_t imp = __ballot(lb != best);
+        if (imp) {
+            uint64_t m = ~0ull;
+            int w = 0;
+            while (imp) {
+                const int i = __ffsll(static_cast<unsigned long long>(imp)) - 1;
+                imp &= imp - 1;
+                const uint64_t ki = coop_key(lane_val(lt, i), lane_val(lb, i));
+                if (ki < m) m = ki, w = i;
+            }
+            best_t = lane_val(lt, w), best = lane_val(lb, w), best_u = lane_val(lu, w), best_v = lane_val(lv, w);
+        }
+        const uint64_t has = __ballot(lnk != kEmptyLinkDev);
+        const int n = popc64(has);
+        if (sp + n > cap) {
+            ok = false;
+        } else {
+            if (lnk != kEmptyLinkDev) *stk.at(sp + lanes_below(has)) = u32x2{lnk, __float_as_uint(key)};
+            sp += n;
+        }
+    }
+    return ok;
+}
+#endif
+
 // BATCH: coop_leaf (a leaf's triangle loads issued together, 48 more live
 // registers) rather than wleaf_tests.
 template <bool SLACK, bool BATCH = true>
 __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, const RayInv& ri, float bound,
                                              CoopStack stk, int cap, float& best_t, int& best, float& best_u,
                                              float& best_v, uint32_t* rounds = nullptr, const RootLds* rl = nullptr) {
+#if BDPT_COOP_CP && !BDPT_QNODES
+    (void)rl;  // (the block's LDS copy of the root: not read by the 4-lane entries)
+    return coop_closest_cp<SLACK>(sc, r, ri, bound, stk, cap, best_t, best, best_u, best_v, rounds);
+#endif
     const uint32_t lane = __lane_id();
     best_t = bound < r.max_t ? bound : r.max_t, best = -1, best_u = best_v = 0.f;
     if (lane == 0) *stk.at(0) = u32x2{sc.wroot_link, __float_as_uint(-__builtin_inff())};
@@ -1563,10 +1692,10 @@ __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, 
             while (imp) {
                 const int i = __ffsll(static_cast<unsigned long long>(imp)) - 1;
                 imp &= imp - 1;
-                const uint64_t ki = coop_key(__shfl(lt, i), __shfl(lb, i));
+                const uint64_t ki = coop_key(lane_val(lt, i), lane_val(lb, i));
                 if (ki < m) m = ki, w = i;
             }
-            best_t = __shfl(lt, w), best = __shfl(lb, w), best_u = __shfl(lu, w), best_v = __shfl(lv, w);
+            best_t = lane_val(lt, w), best = lane_val(lb, w), best_u = lane_val(lu, w), best_v = lane_val(lv, w);
         }
         // children far-first, so the nearest are popped first
 #pragma unroll
@@ -1593,11 +1722,73 @@ __device__ __forceinline__ bool coop_closest(const TravScene& sc, const Ray& r, 
 // (t, index) over the group's candidates); false for a group whose entries did
 // not fit. For the Russian-roulette build's express waves holding 2-4 long walks,
 // which otherwise take turns with all 64 lanes.
+#ifndef BDPT_COOP_GROUPS_CP
+#define BDPT_COOP_GROUPS_CP 1  // coop_closest_groups with coop_closest_cp's 4 lanes per entry (G / 4 entries per round)
+#endif
+#if BDPT_COOP_CP && BDPT_COOP_GROUPS_CP && !BDPT_QNODES
+// coop_closest_groups in coop_closest_cp's layout: group g's lane 4s + c takes child
+// c (or triangles c, c + 4) of the group's entry s, G / 4 entries per round; the
+// same per-entry tests and per-group minimum, so each group's result is
+// coop_closest's for its ray.
+template <bool SLACK>
+__device__ __forceinline__ bool coop_closest_groups_cp(const TravScene& sc, const Ray& r, const RayInv& ri,
+                                                       float bound, bool active, CoopStack stk, int base, int cap,
+                                                       int G, float& best_t, int& best, float& best_u, float& best_v) {
+    const uint32_t lane = __lane_id();
+    const int gl = static_cast<int>(lane) & (G - 1);
+    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (static_cast<int>(lane) - gl);
+    const int slot = gl >> 2, c = gl & 3, per = G >> 2;
+    const f3 oi = SLACK || !BDPT_SLAB_FMA ? mk(0.f, 0.f, 0.f) : slab_fma_origin(r.o, ri.inv);
+    best_t = bound < r.max_t ? bound : r.max_t, best = -1, best_u = best_v = 0.f;
+    if (active && gl == 0) *stk.at(base) = u32x2{sc.wroot_link, __float_as_uint(-__builtin_inff())};
+    int sp = active ? 1 : 0;
+    bool ok = true;
+    while (__ballot(sp > 0)) {
+        const int k = sp < per ? sp : per;
+        u32x2 e = {kEmptyLinkDev, 0u};
+        if (slot < k) e = *stk.at(base + sp - k + slot);
+        sp -= k;
+        const float far = cull_far(best_t);
+        const bool live = e.x != kEmptyLinkDev && !(__uint_as_float(e.y) > far);
+        float lt = best_t, lu = best_u, lv = best_v;
+        int lb = best;
+        float key = __builtin_inff();
+        uint32_t lnk = kEmptyLinkDev;
+        if (live) coop_entry_cp<SLACK>(sc, r, ri, oi, far, e.x, c, lt, lb, lu, lv, key, lnk);
+        // each group's lexicographic minimum of (t, index) over its improving lanes
+        uint64_t imp = __ballot(lb != best);
+        if (imp) {
+            uint64_t m = ~0ull;
+            int w = static_cast<int>(lane);
+            while (imp) {
+                const int i = __ffsll(static_cast<unsigned long long>(imp)) - 1;
+                imp &= imp - 1;
+                const uint64_t ki = coop_key(lane_val(lt, i), lane_val(lb, i));
+                if ((gmask >> i) & 1ull && ki < m) m = ki, w = i;
+            }
+            best_t = __shfl(lt, w), best = __shfl(lb, w), best_u = __shfl(lu, w), best_v = __shfl(lv, w);
+        }
+        const uint64_t has = __ballot(lnk != kEmptyLinkDev) & gmask;
+        const int n = popc64(has);
+        if (sp + n > cap) {
+            ok = false;
+        } else {
+            if (lnk != kEmptyLinkDev) *stk.at(base + sp + lanes_below(has)) = u32x2{lnk, __float_as_uint(key)};
+            sp += n;
+        }
+    }
+    return ok;
+}
+#endif
 template <bool SLACK>
 __device__ __forceinline__ bool coop_closest_groups(const TravScene& sc, const Ray& r, const RayInv& ri, float bound,
                                                     bool active, CoopStack stk, int base, int cap, int G,
                                                     float& best_t, int& best, float& best_u, float& best_v,
                                                     const RootLds* rl = nullptr) {
+#if BDPT_COOP_CP && BDPT_COOP_GROUPS_CP && !BDPT_QNODES
+    (void)rl;
+    return coop_closest_groups_cp<SLACK>(sc, r, ri, bound, active, stk, base, cap, G, best_t, best, best_u, best_v);
+#endif
     const uint32_t lane = __lane_id();
     const int gl = static_cast<int>(lane) & (G - 1);
     const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (static_cast<int>(lane) - gl);
@@ -1632,7 +1823,7 @@ __device__ __forceinline__ bool coop_closest_groups(const TravScene& sc, const R
             while (imp) {
                 const int i = __ffsll(static_cast<unsigned long long>(imp)) - 1;
                 imp &= imp - 1;
-                const uint64_t ki = coop_key(__shfl(lt, i), __shfl(lb, i));
+                const uint64_t ki = coop_key(lane_val(lt, i), lane_val(lb, i));
                 if ((gmask >> i) & 1ull && ki < m) m = ki, w = i;
             }
             best_t = __shfl(lt, w), best = __shfl(lb, w), best_u = __shfl(lu, w), best_v = __shfl(lv, w);

@@ -268,14 +268,14 @@ __device__ __noinline__ int express_chain(Lane& Lcaller, int b, RayInv& ri_calle
     int bounced = -1;
     for (;;) {
         Ray q;
-        q.o = mk(__shfl(L.ray.o.x, b), __shfl(L.ray.o.y, b), __shfl(L.ray.o.z, b));
-        q.d = mk(__shfl(L.ray.d.x, b), __shfl(L.ray.d.y, b), __shfl(L.ray.d.z, b));
-        q.min_t = __shfl(L.ray.min_t, b), q.max_t = __shfl(L.ray.max_t, b);
+        q.o = mk(lane_val(L.ray.o.x, b), lane_val(L.ray.o.y, b), lane_val(L.ray.o.z, b));
+        q.d = mk(lane_val(L.ray.d.x, b), lane_val(L.ray.d.y, b), lane_val(L.ray.d.z, b));
+        q.min_t = lane_val(L.ray.min_t, b), q.max_t = lane_val(L.ray.max_t, b);
         RayInv qi;
-        qi.inv = mk(__shfl(ri.inv.x, b), __shfl(ri.inv.y, b), __shfl(ri.inv.z, b));
-        qi.near = __shfl(ri.near, b);
+        qi.inv = mk(lane_val(ri.inv.x, b), lane_val(ri.inv.y, b), lane_val(ri.inv.z, b));
+        qi.near = lane_val(ri.near, b);
         qi.fast = true;
-        const float guess = BDPT_GRAZE_IN_DIST ? -1.f : __shfl(L.h.dist, b);
+        const float guess = BDPT_GRAZE_IN_DIST ? -1.f : lane_val(L.h.dist, b);
         r = -1;
         ok = true;
         for (int pass = guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
@@ -310,7 +310,7 @@ __device__ __noinline__ int express_chain(Lane& Lcaller, int b, RayInv& ri_calle
                 }
             }
         }
-        more = __shfl(more, b);
+        more = lane_val(more, b);
         if (more == 1) continue;
         bounced = more;
         break;
@@ -610,7 +610,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 chunk_x397 = mt_x397(sample_seed(base + (opaque_tid() & 63), P->fr, px));
 #if BDPT_EYE_SLOTS
                 // the chunk's pixel when all 64 samples share one (spp a multiple of 64)
-                const int cpx = __shfl(px, 0);
+                const int cpx = lane_val(px, 0);
                 if (lane0())
                     eye_slot_reset(P->fb, static_cast<int>(chunk_seq % BDPT_EYE_SLOTS), P->fr.spp % 64 == 0 ? cpx : -1);
                 chunk_seq++;
@@ -822,15 +822,15 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
 #endif
                 for (;;) {
                     Ray q;
-                    q.o = mk(__shfl(L.ray.o.x, b), __shfl(L.ray.o.y, b), __shfl(L.ray.o.z, b));
-                    q.d = mk(__shfl(L.ray.d.x, b), __shfl(L.ray.d.y, b), __shfl(L.ray.d.z, b));
-                    q.min_t = __shfl(L.ray.min_t, b), q.max_t = __shfl(L.ray.max_t, b);
+                    q.o = mk(lane_val(L.ray.o.x, b), lane_val(L.ray.o.y, b), lane_val(L.ray.o.z, b));
+                    q.d = mk(lane_val(L.ray.d.x, b), lane_val(L.ray.d.y, b), lane_val(L.ray.d.z, b));
+                    q.min_t = lane_val(L.ray.min_t, b), q.max_t = lane_val(L.ray.max_t, b);
                     RayInv qi;
-                    qi.inv = mk(__shfl(ri.inv.x, b), __shfl(ri.inv.y, b), __shfl(ri.inv.z, b));
-                    qi.near = __shfl(ri.near, b);
+                    qi.inv = mk(lane_val(ri.inv.x, b), lane_val(ri.inv.y, b), lane_val(ri.inv.z, b));
+                    qi.near = lane_val(ri.near, b);
                     qi.fast = true;
                     // the lane's last hit distance (Hit::dist, shade_hit), the bound's guess
-                    const float guess = BDPT_GRAZE_IN_DIST ? -1.f : __shfl(L.h.dist, b);
+                    const float guess = BDPT_GRAZE_IN_DIST ? -1.f : lane_val(L.h.dist, b);
                     r = -1;
                     ok = true;
                     for (int pass = guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
@@ -874,7 +874,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                             }
                         }
                     }
-                    more = __shfl(more, b);
+                    more = lane_val(more, b);
                     if (more == 1) continue;  // the next bounce's walk, by the whole wave
                     bounced = more;
                     break;
@@ -1238,10 +1238,10 @@ __global__ __launch_bounds__(64) void bdpt_chain_kernel(const KParams* __restric
             const uint64_t c0 = BDPT_CHAIN_PROBE ? __builtin_amdgcn_s_memtime() : 0;
             // lane 0's query, walked by the wave
             Ray q;
-            q.o = mk(__shfl(L.ray.o.x, 0), __shfl(L.ray.o.y, 0), __shfl(L.ray.o.z, 0));
-            q.d = mk(__shfl(L.ray.d.x, 0), __shfl(L.ray.d.y, 0), __shfl(L.ray.d.z, 0));
-            q.min_t = __shfl(L.ray.min_t, 0), q.max_t = __shfl(L.ray.max_t, 0);
-            const float near = __shfl(lane == 0 ? cull_near_for(L) : 0.f, 0);
+            q.o = mk(lane_val(L.ray.o.x, 0), lane_val(L.ray.o.y, 0), lane_val(L.ray.o.z, 0));
+            q.d = mk(lane_val(L.ray.d.x, 0), lane_val(L.ray.d.y, 0), lane_val(L.ray.d.z, 0));
+            q.min_t = lane_val(L.ray.min_t, 0), q.max_t = lane_val(L.ray.max_t, 0);
+            const float near = lane_val(lane == 0 ? cull_near_for(L) : 0.f, 0);
             if (q.min_t > q.max_t) break;  // the megakernel resolves it (a miss)
             const RayInv ri = ray_inv(q, near);
             if (!ri.fast || far_origin(sc, q.o)) break;  // the reference's tree: the megakernel walks it
@@ -1292,7 +1292,7 @@ __global__ __launch_bounds__(64) void bdpt_chain_kernel(const KParams* __restric
                     finish<false>(L, fr, kp.fb, cnt);  // L.state = ST_IDLE
                 }
             }
-            if (!__shfl(more, 0)) break;
+            if (!lane_val(more, 0)) break;
         }
         if (lane == 0) {
             park_save(rec, L);

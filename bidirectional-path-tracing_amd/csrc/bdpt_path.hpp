@@ -861,6 +861,9 @@ __device__ uint32_t advance(Lane& L, uint32_t act, const DevScene& sc, const Dev
 #undef BDPT_BODY_CONTINUE
 #undef BDPT_BODY_LIGHT_NEXT
 
+#ifndef BDPT_SCAN_BITS
+#define BDPT_SCAN_BITS 1  // conn_batch's prefix sum by ballots per bit of the counts (0: six __shfl_up steps)
+#endif
 #if BDPT_HELP && !BDPT_SAMPLER_STATE
 // connectVertices of every owner lane that reached A_CONN in this shading step
 // (bdpt.h:434-483, all its remaining light vertices), flattened over the wave:
@@ -878,13 +881,24 @@ __device__ __forceinline__ void conn_batch(Lane& L, bool owner, const DevScene& 
     const uint64_t om = __ballot(k > 0);
     if (!om) return;
     const int me = static_cast<int>(opaque_tid() & 63);
+#if BDPT_SCAN_BITS
+    // exclusive prefix sum of k over the wave, one bit of k at a time: lanes below
+    // with the bit set (mbcnt of a ballot) times its weight — no LDS round trips
+    int excl = 0, total = 0;
+    for (int b = 0, rest = k; __ballot(rest != 0); b++, rest >>= 1) {  // (wave-uniform)
+        const uint64_t m = __ballot(rest & 1);
+        excl += lanes_below(m) << b;
+        total += popc64(m) << b;
+    }
+#else
     int incl = k;  // inclusive prefix sum of k over the wave
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const int t = __shfl_up(incl, off);
         if (me >= off) incl += t;
     }
-    const int total = __shfl(incl, 63), excl = incl - k;
+    const int total = lane_val(incl, 63), excl = incl - k;
+#endif
     {
         const TaskCtl ctl = task_ctl(L.c);
         if (static_cast<uint32_t>(total) > fr.task_cap - (*ctl.tail - *ctl.head)) return;

@@ -69,7 +69,7 @@ abtest)
       --timeout-method thread > gpurun_out/${LABEL}_tests_$lib.log 2>&1
     rc=$?
     tail -1 gpurun_out/${LABEL}_tests_$lib.log
-    [ $rc -ne 0 ] && exit $rc
+    if [ $rc -ne 0 ]; then exit $rc; fi
   done
   ;;
 ab)
