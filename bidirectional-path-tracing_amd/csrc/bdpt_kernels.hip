@@ -508,7 +508,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
     // shading step (the frame cannot end before it does).
     bool long_walk = false;
 #if BDPT_EXPRESS_PROBE
-    uint64_t xp_iters = 0, xp_coop = 0, xp_total = 0, xp_t = 0;  // (wave-uniform)
+    uint64_t xp_iters = 0, xp_coop = 0, xp_total = 0, xp_t = 0, xp_walk = 0;  // (wave-uniform)
     bool xp_prev = false;
 #endif
 #if BDPT_HELP
@@ -833,6 +833,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     const float guess = BDPT_GRAZE_IN_DIST ? -1.f : lane_val(L.h.dist, b);
                     r = -1;
                     ok = true;
+#if BDPT_EXPRESS_PROBE
+                    const uint64_t xw0 = __builtin_amdgcn_s_memtime();
+#endif
                     for (int pass = guess > 0.f ? 0 : 1; pass < 2 && r < 0 && ok; pass++) {
                         const float bound = pass == 0 ? 2.f * guess : q.max_t;
                         ok = SLACK ? coop_closest<true, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v,
@@ -840,6 +843,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                                    : coop_closest<false, BDPT_COOP_BATCH>(tsc, q, qi, bound, cs, 64 * kLdsStack, t, r, u, v,
                                                                           nullptr, coop_rl);
                     }
+#if BDPT_EXPRESS_PROBE
+                    if (xp_lone) xp_walk += __builtin_amdgcn_s_memtime() - xw0;
+#endif
                     if (BDPT_EXPRESS_CHAIN != 1 || !chain || !ok) break;
                     int more = -1;  // (lane b) -1: not a delta bounce; 0: the chain ended; 1: next bounce here; 2: at the loop top
                     if (me == b && r >= 0 && t <= L.ray.max_t && t >= L.ray.min_t) {  // accel.h:133
@@ -1158,6 +1164,7 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
         gadd(kpp->counters + kCounters + 3, static_cast<unsigned long long>(xp_iters));
         gadd(kpp->counters + kCounters + 3 + 1, static_cast<unsigned long long>(xp_coop));
         gadd(kpp->counters + kCounters + 3 + 2, static_cast<unsigned long long>(xp_total));
+        gadd(kpp->counters + kCounters + 3 + 3, static_cast<unsigned long long>(xp_walk));  // of xp_coop: in the walks
     }
 #endif
 #if BDPT_TAIL_PROBE && BDPT_RR != 1
