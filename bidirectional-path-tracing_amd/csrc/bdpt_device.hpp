@@ -433,6 +433,31 @@ __device__ BDPT_NOINLINE bool mt_ring_ahead(const LazyMT& r) {
     if (moved) ring[624] = xa0, ring[625] = xa1, ring[626] = g;
     return true;
 }
+// The wave generates lane b's ring ahead (the Russian-roulette build's inline
+// chain: one lane draws while 63 wait): outputs g .. n + 63, lane j computing
+// output g + j from the three words it reads. Every lane reads before any lane
+// writes (each store waits on the wave's loads), and fewer than 227 consecutive
+// outputs never read one another, so the words are mt_ring_ahead's; only once
+// output 624 is past (no seeding values left). n and a0 are lane b's (wave-
+// uniform). Returns the outputs generated so far, or 0 when lane b's ring is not
+// its own or not that far (lane b then calls mt_ring_ahead, which reports it).
+__device__ __forceinline__ uint32_t mt_ring_ahead_wave(int b, uint32_t n, uint32_t a0) {
+    const uint64_t base = (static_cast<uint64_t>(g_scene_lds[1]) << 32) | g_scene_lds[0];
+    uint32_t* const ring =
+        reinterpret_cast<uint32_t*>(base) + static_cast<size_t>(g_scene_lds[3] + (threadIdx.x & ~63u) + b) * kMtRingWords;
+    const uint32_t g = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(ring[626])));
+    const uint32_t tag = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(ring[628])));
+    if (tag != a0 || g < n || g < 624) return 0;
+    const uint32_t want = n + 64;
+    if (g >= want) return g;
+    const uint32_t gj = g + __lane_id();
+    uint32_t v = 0;
+    if (gj < want) v = mt_twist(ring[(gj - 624) % 624], ring[(gj - 623) % 624], ring[(gj - 227) % 624]);
+    if (gj < want) ring[gj % 624] = v;
+    if (__lane_id() == 0) ring[626] = want;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // (the stores done before lane b reads them)
+    return want;
+}
 __device__ __forceinline__ uint32_t mt_u32_long(LazyMT& r) {
     const uint32_t v = mt_ring_slot()[r.n % 624];
     r.n++;

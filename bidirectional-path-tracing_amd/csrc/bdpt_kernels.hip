@@ -381,6 +381,13 @@ struct KParams {
 #ifndef BDPT_EXPRESS_CHAIN
 #define BDPT_EXPRESS_CHAIN 0  // RR build: a lone long walk's delta bounces back to back inside the express block
 #endif
+#ifndef BDPT_CHAIN_RING_WAVE
+#define BDPT_CHAIN_RING_WAVE 1  // the inline chain's generator ring refilled by the whole wave (mt_ring_ahead_wave)
+#endif
+#if !(BDPT_EXPRESS_CHAIN == 1 && BDPT_DEEP_RNG && BDPT_RING_AHEAD)
+#undef BDPT_CHAIN_RING_WAVE
+#define BDPT_CHAIN_RING_WAVE 0
+#endif
 #ifndef BDPT_EXPRESS_PROBE
 #define BDPT_EXPRESS_PROBE 0  // measurement only (RR build): express waves with one busy lane, clocks per iteration and in the coop walk
 #endif
@@ -814,6 +821,9 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                 // took ~40 % of each bounce's clocks (round 6 probe, BDPT_EXPRESS_PROBE).
                 const bool chain = BDPT_EXPRESS_CHAIN && popc64(busy) == 1;
                 int bounced = -1;  // -1: the result goes to the sweep; 0: the chain ended here; 2: its next query begins at the loop top
+#if BDPT_CHAIN_RING_WAVE
+                uint32_t chain_g = 0;  // lane b's ring outputs generated, as the wave last left it (0: unknown)
+#endif
 #if BDPT_EXPRESS_CHAIN == 2
                 if (chain) {
                     bounced = express_chain<SLACK>(L, b, ri, P->sc, P->fr, P->fb, tsc, stack_mem + (threadIdx.x & ~63u),
@@ -847,6 +857,13 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                     if (xp_lone) xp_walk += __builtin_amdgcn_s_memtime() - xw0;
 #endif
                     if (BDPT_EXPRESS_CHAIN != 1 || !chain || !ok) break;
+#if BDPT_CHAIN_RING_WAVE
+                    if (chain) {  // lane b's generator ring, refilled by the wave when its next bounce could reach the end
+                        const uint32_t bn = static_cast<uint32_t>(lane_val(static_cast<int>(L.rng.n), b));
+                        if (bn + BDPT_RING_AHEAD >= chain_g)
+                            chain_g = mt_ring_ahead_wave(b, bn, static_cast<uint32_t>(lane_val(static_cast<int>(L.rng.a0), b)));
+                    }
+#endif
                     int more = -1;  // (lane b) -1: not a delta bounce; 0: the chain ended; 1: next bounce here; 2: at the loop top
                     if (me == b && r >= 0 && t <= L.ray.max_t && t >= L.ray.min_t) {  // accel.h:133
                         const BsdfRecord& bb =
@@ -862,7 +879,12 @@ __global__ __launch_bounds__(kBlock, BDPT_WAVES_PER_EU) void bdpt_frame_kernel(c
                             BDPT_DIST_TO_GRAZE
                             const float absCosIn = fabsf(L.h.wo.z);
 #if BDPT_DEEP_RNG && BDPT_RING_AHEAD
-                            if (L.rng.n + BDPT_RING_AHEAD >= 227 && !mt_ring_ahead(L.rng) && P->fr.diag)
+#if BDPT_CHAIN_RING_WAVE
+                            const bool ring_ok = chain_g >= L.rng.n + BDPT_RING_AHEAD;  // the wave generated far enough
+#else
+                            constexpr bool ring_ok = false;
+#endif
+                            if (L.rng.n + BDPT_RING_AHEAD >= 227 && !ring_ok && !mt_ring_ahead(L.rng) && P->fr.diag)
                                 gadd(P->fr.diag + kDiagErrors, 1ull);
 #endif
                             L.c.vcm *= div_w(dist2, absCosIn);

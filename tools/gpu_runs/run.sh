@@ -92,7 +92,7 @@ ab)
 profile)
   timeout -k 10 900 bash tools/profile_round.sh $LABEL "$@"
   ;;
-final|final_a|final_b|final_c|final_tc|final_pc)
+final|final_a|final_b|final_c|final_tc|final_pc|final_ac)
   P=gpurun_out/prof_$LABEL
   kt() {  # name limit bench args...: the bench line under the kernel trace
     local name=$1 lim=$2; shift 2
@@ -123,6 +123,7 @@ final|final_a|final_b|final_c|final_tc|final_pc)
   final_a) tools/gpu_steps.sh "${A[@]}" ;;
   final_c) tools/gpu_steps.sh "${C[@]}" ;;
   final_tc) tools/gpu_steps.sh "${A[0]}" "${A[1]}" "${C[@]}" ;;  # (suite + smoke, then final_c)
+  final_ac) tools/gpu_steps.sh "${A[@]}" "${C[@]}" ;;  # (final_a then final_c)
   final_pc) tools/gpu_steps.sh "${A[1]}" "${A[2]}" "${A[3]}" "${C[@]}" ;;  # (smoke and all four profiles: the suite ran on the build already)
   final_b) tools/gpu_steps.sh "${B[@]}" ;;
   esac
